@@ -1,0 +1,83 @@
+/*
+ * orb_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference ORB front end, used as the parity checker for the
+ * HIP path (tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg only; the
+ * product never links, loads or calls it).  See orb_oracle.cpp's header for what is
+ * restated from where and how each un-vendored dependency is pinned.
+ */
+#ifndef ORB_ORACLE_H
+#define ORB_ORACLE_H
+
+#include <stdint.h>
+
+#include "../include/orb_abi.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct oracle_extractor oracle_extractor_t;
+
+oracle_extractor_t* oracle_extractor_create(int nfeatures, float scale_factor, int nlevels, int score_type,
+                                            int fast_th);
+void oracle_extractor_destroy(oracle_extractor_t* h);
+int oracle_get_level_info(const oracle_extractor_t* h, int* features_per_level, float* scale_factors,
+                          float* inv_scale_factors, int* umax16);
+/* ORBextractor::operator() on one image; returns status, *n_out keypoints. */
+int oracle_extract(oracle_extractor_t* h, const uint8_t* img, int w, int hgt, int stride, orb_keypoint_t* kps,
+                   int cap, uint8_t* desc, int* n_out);
+/* After oracle_extract: padded (w+32)x(h+32) level `l` BEFORE the descriptor blur. */
+int oracle_level_image(const oracle_extractor_t* h, int l, uint8_t* out, int* w, int* hgt);
+/* After oracle_extract: the blurred ROI of level l (w x h), as the descriptors read it. */
+int oracle_level_blurred(const oracle_extractor_t* h, int l, uint8_t* out);
+/* After oracle_extract: per-cell FAST counts nTotal (row-major cells) of level l. */
+int oracle_cell_counts(const oracle_extractor_t* h, int l, int* rows, int* cols, int* counts, int cap);
+
+/* Primitives, exposed for unit tests. */
+float oracle_fast_atan2(float y, float x);
+float oracle_sinf(float x);
+float oracle_cosf(float x);
+int oracle_descriptor_distance(const uint8_t* a, const uint8_t* b);
+/* libstdc++ nth_element on float responses (greater): permutes idx[] of length n by keys. */
+void oracle_nth_element_greater(const float* keys, int32_t* idx, int n, int nth);
+/* OpenCV 2.4 getGaussianKernel(7, 2, CV_32F) * 256 -> int (the blur's fixed-point taps). */
+void oracle_gaussian_taps(int* taps7);
+
+int oracle_search_for_initialization(const orb_keypoint_t* kps1, const uint8_t* desc1, int n1,
+                                     const orb_keypoint_t* kps2, const uint8_t* desc2, int n2,
+                                     orb_frame_bounds_t bounds, float nnratio, int check_ori, int window,
+                                     float* prev_xy, int32_t* matches12, int* n_matches);
+
+/* Frame::GetFeaturesInArea on a frame built from kps (reference Frame.cc:200-265). */
+int oracle_features_in_area(const orb_keypoint_t* kps, int n, orb_frame_bounds_t bounds, float x, float y, float r,
+                            int min_level, int max_level, int32_t* out, int cap);
+
+/* SearchByBoW(KeyFrame*, Frame&) (ORBmatcher.cc:155-284).  FeatureVectors as CSR:
+ * sorted node ids nodes[nn], offsets off[nn+1], feature indices feat[off[nn]].
+ * kf_valid[i]: KF keypoint i has a non-bad MapPoint.  out_match[N_F]: KF feature index
+ * whose MapPoint was assigned to F keypoint j, or -1. */
+int oracle_search_by_bow_kf_f(const orb_keypoint_t* kf_kps, const uint8_t* kf_desc, int n_kf,
+                              const uint8_t* kf_valid, const uint32_t* kf_nodes, const int32_t* kf_off,
+                              const int32_t* kf_feat, int kf_nn, const orb_keypoint_t* f_kps, const uint8_t* f_desc,
+                              int n_f, const uint32_t* f_nodes, const int32_t* f_off, const int32_t* f_feat, int f_nn,
+                              float nnratio, int check_ori, int32_t* out_match, int* n_matches);
+
+/* SearchByBoW(KeyFrame*, KeyFrame*) (ORBmatcher.cc:715-850); out_match[n1] = idx2 or -1. */
+int oracle_search_by_bow_kf_kf(const orb_keypoint_t* kps1, const uint8_t* desc1, int n1, const uint8_t* valid1,
+                               const uint32_t* nodes1, const int32_t* off1, const int32_t* feat1, int nn1,
+                               const orb_keypoint_t* kps2, const uint8_t* desc2, int n2, const uint8_t* valid2,
+                               const uint32_t* nodes2, const int32_t* off2, const int32_t* feat2, int nn2,
+                               float nnratio, int check_ori, int32_t* out_match, int* n_matches);
+
+/* CPU baseline: extract B frames (frame k at imgs + k*pitch) with `threads` workers (one
+ * extractor per worker, frames round-robin) and, if match != 0, SearchForInitialization on
+ * consecutive pairs (2k, 2k+1) with window 100.  Returns wall seconds (< 0 on error). */
+double oracle_bench(int nfeatures, float scale_factor, int nlevels, int fast_th, const uint8_t* imgs, int B, int w,
+                    int hgt, int stride, int64_t pitch, int threads, int match, int64_t* total_kps,
+                    int64_t* total_matches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

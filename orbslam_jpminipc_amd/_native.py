@@ -1,0 +1,142 @@
+"""ctypes bindings to the in-tree native libraries.
+
+``liborb_hip.so`` is the product (HIP kernels + the C ABI of ``include/orb_abi.h``);
+``libsynth.so`` is the host-only synthetic frame generator.  Both are built in-tree by
+``__graft_entry__.build()``.  There is no CPU fallback: if the HIP library is missing or
+cannot be loaded, every entry point raises ``NativeLibraryError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import pathlib
+
+import numpy as np
+
+PKG_DIR = pathlib.Path(__file__).resolve().parent
+HIP_LIB_PATH = PKG_DIR / "liborb_hip.so"
+SYNTH_LIB_PATH = PKG_DIR / "libsynth.so"
+
+# cv::KeyPoint layout (28 bytes), reference include/SaveLoadWorld.h:1406-1425
+KEYPOINT_DTYPE = np.dtype(
+    [
+        ("x", "<f4"),
+        ("y", "<f4"),
+        ("size", "<f4"),
+        ("angle", "<f4"),
+        ("response", "<f4"),
+        ("octave", "<i4"),
+        ("class_id", "<i4"),
+    ]
+)
+assert KEYPOINT_DTYPE.itemsize == 28
+
+ORB_OK = 0
+ORB_EINVAL = -22
+ORB_ENOMEM = -12
+ORB_ERANGE = -34
+ORB_EDEVICE = -5
+ORB_ENOTSUP = -95
+
+HARRIS_SCORE = 0
+FAST_SCORE = 1
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+class OrbError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"orb status {code}: {msg}")
+        self.code = code
+
+
+class FrameBounds(ctypes.Structure):
+    _fields_ = [("min_x", ctypes.c_int), ("max_x", ctypes.c_int), ("min_y", ctypes.c_int), ("max_y", ctypes.c_int)]
+
+
+_vp = ctypes.c_void_p
+_i = ctypes.c_int
+_i64 = ctypes.c_int64
+_f = ctypes.c_float
+
+# name -> (restype, argtypes); every symbol declared in include/orb_abi.h
+HIP_SIGNATURES = {
+    "orb_last_error": (ctypes.c_char_p, []),
+    "orb_version": (ctypes.c_char_p, []),
+    "orb_extractor_create": (_i, [_i, _f, _i, _i, _i, _i, _i, ctypes.POINTER(_vp)]),
+    "orb_extractor_destroy": (_i, [_vp]),
+    "orb_get_levels": (_i, [_vp]),
+    "orb_get_scale_factor": (_f, [_vp]),
+    "orb_get_max_keypoints": (_i, [_vp]),
+    "orb_get_level_info": (_i, [_vp, _vp, _vp]),
+    "orb_extract": (_i, [_vp, _vp, _i, _i, _i, _vp, _i, _vp, ctypes.POINTER(_i)]),
+    "orb_extract_batch_device": (_i, [_vp, _i, _vp, _i, _i, _i, _i64, _vp, _vp, _vp, _vp]),
+    "orb_extract_batch": (_i, [_vp, _i, _vp, _i, _i, _i, _i64, _vp, _vp, _vp]),
+    "orb_descriptor_distance": (_i, [_vp, _vp]),
+    "orb_search_for_initialization": (
+        _i,
+        [_vp, _vp, _i, _vp, _vp, _i, FrameBounds, _f, _i, _i, _vp, _vp, ctypes.POINTER(_i)],
+    ),
+    "orb_search_for_initialization_batch_device": (
+        _i,
+        [_vp, _vp, _vp, _i, _i, _vp, _vp, FrameBounds, _f, _i, _i, _vp, _vp, _vp, _vp],
+    ),
+    "orb_debug_nth_element_u32": (_i, [_vp, _i, _i]),
+    "orb_debug_level_image": (_i, [_vp, _i, _i, _vp, ctypes.POINTER(_i), ctypes.POINTER(_i)]),
+    "orb_debug_cell_counts": (_i, [_vp, _i, _i, _vp, _i]),
+}
+
+_hip = None
+_synth = None
+
+
+def hip_lib() -> ctypes.CDLL:
+    """Load liborb_hip.so (fails loudly: there is no CPU fallback)."""
+    global _hip
+    if _hip is None:
+        if not HIP_LIB_PATH.exists():
+            raise NativeLibraryError(
+                f"{HIP_LIB_PATH} is missing; run `python -c 'import __graft_entry__ as g; g.build()'`"
+            )
+        try:
+            lib = ctypes.CDLL(str(HIP_LIB_PATH), mode=os.RTLD_LOCAL)
+        except OSError as e:  # pragma: no cover - environment dependent
+            raise NativeLibraryError(f"cannot load {HIP_LIB_PATH}: {e}") from e
+        for name, (res, args) in HIP_SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _hip = lib
+    return _hip
+
+
+def synth_lib() -> ctypes.CDLL:
+    global _synth
+    if _synth is None:
+        if not SYNTH_LIB_PATH.exists():
+            raise NativeLibraryError(f"{SYNTH_LIB_PATH} is missing; run __graft_entry__.build()")
+        lib = ctypes.CDLL(str(SYNTH_LIB_PATH))
+        lib.orb_synth_stream.restype = _i
+        lib.orb_synth_stream.argtypes = [_i, _i, ctypes.c_uint64, ctypes.c_uint64, _i, _vp, _i, _i64]
+        lib.orb_synth_special.restype = _i
+        lib.orb_synth_special.argtypes = [_i, _i, _i, ctypes.c_uint64, _vp, _i]
+        _synth = lib
+    return _synth
+
+
+def check(code: int) -> int:
+    if code < 0:
+        msg = hip_lib().orb_last_error()
+        raise OrbError(code, msg.decode() if msg else "")
+    return code
+
+
+def ptr(a) -> ctypes.c_void_p:
+    """Data pointer of a numpy array or torch tensor."""
+    if a is None:
+        return ctypes.c_void_p(0)
+    if isinstance(a, np.ndarray):
+        return ctypes.c_void_p(a.ctypes.data)
+    return ctypes.c_void_p(a.data_ptr())

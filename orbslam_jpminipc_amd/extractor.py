@@ -1,0 +1,128 @@
+"""ORBextractor — host mirror of the reference class over the HIP C ABI.
+
+Reference: include/ORBextractor.h:30-80, src/ORBextractor.cc:457-822.  Same constructor
+arguments and defaults, same ``operator()`` semantics (``__call__`` here):
+
+* an empty image returns without producing outputs (ORBextractor.cc:721-722) — here
+  ``(None, None)``;
+* a non-empty image yields N <= nfeatures keypoints (cv::KeyPoint records,
+  ``KEYPOINT_DTYPE``) and an N x 32 uint8 descriptor matrix, or ``None`` descriptors when
+  N == 0 (``_descriptors.release()``, ORBextractor.cc:738-739);
+* the mask argument is accepted and ignored, as the reference's FAST ignores it.
+
+All arithmetic runs in the HIP kernels of csrc/orb_hip.hip; this module only marshals.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from ._native import FAST_SCORE, HARRIS_SCORE, KEYPOINT_DTYPE, check, hip_lib, ptr
+
+
+class ORBextractor:
+    HARRIS_SCORE = HARRIS_SCORE
+    FAST_SCORE = FAST_SCORE
+
+    def __init__(
+        self,
+        nfeatures: int = 1000,
+        scaleFactor: float = 1.2,
+        nlevels: int = 8,
+        scoreType: int = FAST_SCORE,
+        fastTh: int = 20,
+        device: int = 0,
+        max_batch: int = 1,
+    ):
+        self._lib = hip_lib()
+        h = ctypes.c_void_p()
+        check(self._lib.orb_extractor_create(nfeatures, scaleFactor, nlevels, scoreType, fastTh, device, max_batch,
+                                             ctypes.byref(h)))
+        self._h = h
+        self.nfeatures = nfeatures
+        self.nlevels = nlevels
+        self.scoreType = scoreType
+        self.fastTh = fastTh
+        self.device = device
+        self.max_batch = max_batch
+        self.max_keypoints = check(self._lib.orb_get_max_keypoints(self._h))
+        fpl = np.zeros(nlevels, np.int32)
+        sf = np.zeros(nlevels, np.float32)
+        check(self._lib.orb_get_level_info(self._h, ptr(fpl), ptr(sf)))
+        self.mnFeaturesPerLevel = fpl
+        self.mvScaleFactor = sf
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._lib.orb_extractor_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ORBextractor::GetLevels / GetScaleFactor (ORBextractor.h:47-51)
+    def GetLevels(self) -> int:
+        return self._lib.orb_get_levels(self._h)
+
+    def GetScaleFactor(self) -> float:
+        return float(self._lib.orb_get_scale_factor(self._h))
+
+    def __call__(self, image, mask=None):
+        img = np.asarray(image)
+        if img.size == 0:
+            return None, None
+        if img.dtype != np.uint8 or img.ndim != 2:
+            raise TypeError("image must be a 2-D uint8 array (CV_8UC1), ORBextractor.cc:725")
+        if img.strides[1] != 1:
+            img = np.ascontiguousarray(img)
+        h, w = img.shape
+        cap = self.max_keypoints
+        kps = np.empty(cap, KEYPOINT_DTYPE)
+        desc = np.empty((cap, 32), np.uint8)
+        n = ctypes.c_int()
+        check(self._lib.orb_extract(self._h, ptr(img), w, h, img.strides[0], ptr(kps), cap, ptr(desc), ctypes.byref(n)))
+        n = n.value
+        return kps[:n].copy(), (desc[:n].copy() if n > 0 else None)
+
+    def extract_batch(self, images: np.ndarray):
+        """B host frames (B, H, W) uint8 -> list of (keypoints, descriptors)."""
+        imgs = np.ascontiguousarray(images, dtype=np.uint8)
+        B, h, w = imgs.shape
+        cap = self.max_keypoints
+        kps = np.empty((B, cap), KEYPOINT_DTYPE)
+        desc = np.empty((B, cap, 32), np.uint8)
+        counts = np.zeros(B, np.int32)
+        check(self._lib.orb_extract_batch(self._h, B, ptr(imgs), w, h, w, w * h, ptr(kps), ptr(desc), ptr(counts)))
+        return [(kps[b, : counts[b]].copy(), desc[b, : counts[b]].copy() if counts[b] else None) for b in range(B)]
+
+    def extract_batch_device(self, d_imgs, d_kps=None, d_desc=None, d_counts=None, stream=None):
+        """Device-resident batch: d_imgs is a (B, H, W) uint8 torch tensor on this device.
+
+        Returns (d_kps (B, cap, 28) uint8, d_desc (B, cap, 32) uint8, d_counts (B,) int32),
+        enqueued on `stream` (a torch.cuda.Stream; default: the current stream).
+        """
+        import torch
+
+        B, h, w = d_imgs.shape
+        cap = self.max_keypoints
+        dev = d_imgs.device
+        if d_kps is None:
+            d_kps = torch.empty((B, cap, 28), dtype=torch.uint8, device=dev)
+        if d_desc is None:
+            d_desc = torch.empty((B, cap, 32), dtype=torch.uint8, device=dev)
+        if d_counts is None:
+            d_counts = torch.empty((B,), dtype=torch.int32, device=dev)
+        s = stream if stream is not None else torch.cuda.current_stream(dev)
+        check(self._lib.orb_extract_batch_device(self._h, B, ptr(d_imgs), w, h, d_imgs.stride(1), d_imgs.stride(0),
+                                                 ptr(d_kps), ptr(d_desc), ptr(d_counts),
+                                                 ctypes.c_void_p(s.cuda_stream)))
+        return d_kps, d_desc, d_counts
+
+
+def keypoints_from_bytes(raw: np.ndarray, n: int) -> np.ndarray:
+    """View n records of a (cap, 28) uint8 buffer as KEYPOINT_DTYPE."""
+    return np.ascontiguousarray(raw[:n]).view(KEYPOINT_DTYPE).reshape(-1)

@@ -1,0 +1,194 @@
+"""GPU parity: the HIP path through the C ABI vs the CPU oracle, bit-exact.
+
+Keypoints are compared as raw 28-byte records (all 7 cv::KeyPoint fields, float bit
+patterns), descriptors byte-by-byte, matches index-by-index.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import orbslam_jpminipc_amd as orb
+from oracle_lib import Oracle, search_for_initialization
+
+pytestmark = pytest.mark.gpu
+
+
+def _diagnose(ext, ora, img, kg, ko):
+    """Localise the first differing stage: pyramid level, then per-cell FAST counts."""
+    lib = orb.hip_lib()
+    lines = []
+    for l in range(ext.nlevels):
+        w, h = ctypes.c_int(), ctypes.c_int()
+        lib.orb_debug_level_image(ext._h, 0, l, None, ctypes.byref(w), ctypes.byref(h))
+        g = np.empty((h.value + 32, w.value + 32), np.uint8)
+        lib.orb_debug_level_image(ext._h, 0, l, g.ctypes.data_as(ctypes.c_void_p), ctypes.byref(w), ctypes.byref(h))
+        o = ora.level_image(l)
+        if g.shape != o.shape or not np.array_equal(g, o):
+            bad = np.argwhere(g != o) if g.shape == o.shape else "shape"
+            lines.append(f"level {l} image differs: {bad[:5] if not isinstance(bad, str) else bad}")
+            break
+        cnt = np.zeros(4096, np.int32)
+        n = lib.orb_debug_cell_counts(ext._h, 0, l, cnt.ctypes.data_as(ctypes.c_void_p), 4096)
+        oc = ora.cell_counts(l).reshape(-1)
+        if n != oc.size or not np.array_equal(cnt[:n], oc):
+            lines.append(f"level {l} cell counts differ: gpu {cnt[:n].tolist()} oracle {oc.tolist()}")
+            break
+    ng, no = len(kg), len(ko)
+    lines.append(f"n gpu {ng} oracle {no}")
+    m = min(ng, no)
+    if m:
+        diff = np.nonzero((kg[:m].view(np.uint8).reshape(m, 28) != ko[:m].view(np.uint8).reshape(m, 28)).any(axis=1))[0]
+        if len(diff):
+            i = diff[0]
+            lines.append(f"first differing keypoint {i}: gpu {kg[i]} oracle {ko[i]}")
+    return "\n".join(lines)
+
+
+def _check_frame(ext, ora, img):
+    kg, dg = ext(img)
+    ko, do = ora.extract(img)
+    if len(kg) != len(ko) or kg.tobytes() != ko.tobytes():
+        pytest.fail("keypoints differ\n" + _diagnose(ext, ora, img, kg, ko))
+    if len(ko) == 0:
+        assert dg is None
+        return kg, dg
+    if dg.tobytes() != do.tobytes():
+        rows = np.nonzero((dg != do).any(axis=1))[0]
+        pytest.fail(f"descriptors differ in {len(rows)} rows, first {rows[:5]}: kp {kg[rows[0]]}")
+    return kg, dg
+
+
+CONFIGS = [
+    # (W, H, nfeatures) — BASELINE.json configs C1/C2, the reference init extractor, C4, C5
+    (640, 480, 1000),
+    (640, 480, 2000),
+    (1241, 376, 2000),
+    (1280, 720, 2500),
+]
+
+
+@pytest.mark.parametrize("W,H,nf", CONFIGS)
+def test_extract_parity_configs(W, H, nf):
+    ext = orb.ORBextractor(nf, 1.2, 8, orb.FAST_SCORE, 20, device=0)
+    ora = Oracle(nf, 1.2, 8, 1, 20)
+    frames = orb.synth_stream(W, H, stream=3, first=0, count=3)
+    for img in frames:
+        _check_frame(ext, ora, img)
+
+
+@pytest.mark.parametrize("W,H", [(320, 240), (641, 479), (752, 480), (161, 121)])
+def test_extract_parity_odd_sizes(W, H):
+    nf = 1000 if W >= 320 else 300
+    ext = orb.ORBextractor(nf, 1.2, 8 if W >= 320 else 4, orb.FAST_SCORE, 20, device=0)
+    ora = Oracle(nf, 1.2, 8 if W >= 320 else 4, 1, 20)
+    for img in orb.synth_stream(W, H, stream=11, first=0, count=2):
+        _check_frame(ext, ora, img)
+
+
+@pytest.mark.parametrize("kind", [orb.SYN_FLAT, orb.SYN_LOWTEX, orb.SYN_NOISE])
+def test_extract_parity_edge_frames(kind):
+    ext = orb.ORBextractor(1000, 1.2, 8, orb.FAST_SCORE, 20, device=0)
+    ora = Oracle(1000, 1.2, 8, 1, 20)
+    img = orb.synth_special(kind, 640, 480, seed=5)
+    kg, dg = _check_frame(ext, ora, img)
+    if kind == orb.SYN_FLAT:
+        assert len(kg) == 0 and dg is None  # _descriptors.release() path
+
+
+def test_extract_parity_fast_thresholds():
+    for th in (7, 12, 35):
+        ext = orb.ORBextractor(1000, 1.2, 8, orb.FAST_SCORE, th, device=0)
+        ora = Oracle(1000, 1.2, 8, 1, th)
+        _check_frame(ext, ora, orb.synth_stream(640, 480, stream=21, count=1)[0])
+
+
+def test_empty_image_returns_untouched():
+    ext = orb.ORBextractor(1000, 1.2, 8, orb.FAST_SCORE, 20, device=0)
+    assert ext(np.zeros((0, 0), np.uint8)) == (None, None)
+
+
+def test_batch_device_equals_single():
+    import torch
+
+    B, W, H = 6, 640, 480
+    frames = orb.synth_stream(W, H, stream=2, first=0, count=B)
+    ext = orb.ORBextractor(1000, 1.2, 8, orb.FAST_SCORE, 20, device=0, max_batch=B)
+    d = torch.from_numpy(frames).cuda()
+    kps, desc, counts = ext.extract_batch_device(d)
+    torch.cuda.synchronize()
+    kps, desc, counts = kps.cpu().numpy(), desc.cpu().numpy(), counts.cpu().numpy()
+    ora = Oracle(1000, 1.2, 8, 1, 20)
+    for b in range(B):
+        ko, do = ora.extract(frames[b])
+        n = counts[b]
+        assert n == len(ko)
+        assert kps[b, :n].tobytes() == ko.tobytes()
+        assert desc[b, :n].tobytes() == do.tobytes()
+    # host-batch entry point too
+    outs = ext.extract_batch(frames)
+    for b in range(B):
+        assert outs[b][0].tobytes() == kps[b, : counts[b]].tobytes()
+
+
+@pytest.mark.parametrize("W,H,nf", [(640, 480, 1000), (640, 480, 2000), (1241, 376, 2000)])
+def test_search_for_initialization_parity(W, H, nf):
+    ext = orb.ORBextractor(nf, 1.2, 8, orb.FAST_SCORE, 20, device=0)
+    frames = orb.synth_stream(W, H, stream=5, first=0, count=4)
+    F = [orb.Frame.from_image(f, ext) for f in frames]
+    matcher = orb.ORBmatcher(0.9, True)
+    for a, b in [(0, 1), (1, 2), (0, 3)]:
+        prev = np.ascontiguousarray(np.stack([F[a].mvKeys["x"], F[a].mvKeys["y"]], 1).astype(np.float32))
+        prev_o = prev.copy()
+        m12 = []
+        n = matcher.SearchForInitialization(F[a], F[b], prev, m12, 100)
+        no, m12o = search_for_initialization(F[a].mvKeys, F[a].mDescriptors, F[b].mvKeys, F[b].mDescriptors, W, H,
+                                             prev_o, 0.9, True, 100)
+        assert n == no
+        assert np.array_equal(np.array(m12, np.int32), m12o)
+        assert prev.tobytes() == prev_o.tobytes()
+        assert n > 0
+        # second call with the updated vbPrevMatched (Tracking::Initialize on the next frame)
+        n2 = matcher.SearchForInitialization(F[a], F[b], prev, m12, 100)
+        no2, m12o2 = search_for_initialization(F[a].mvKeys, F[a].mDescriptors, F[b].mvKeys, F[b].mDescriptors, W, H,
+                                               prev_o, 0.9, True, 100)
+        assert n2 == no2 and np.array_equal(np.array(m12, np.int32), m12o2)
+
+
+@pytest.mark.parametrize("nnratio,checkOri,window", [(0.6, True, 10), (0.9, False, 50), (0.75, True, 200)])
+def test_search_for_initialization_variants(nnratio, checkOri, window):
+    W, H = 640, 480
+    ext = orb.ORBextractor(1000, 1.2, 8, orb.FAST_SCORE, 20, device=0)
+    frames = orb.synth_stream(W, H, stream=9, first=0, count=2)
+    F = [orb.Frame.from_image(f, ext) for f in frames]
+    prev = np.ascontiguousarray(np.stack([F[0].mvKeys["x"], F[0].mvKeys["y"]], 1).astype(np.float32))
+    prev_o = prev.copy()
+    m12 = []
+    n = orb.ORBmatcher(nnratio, checkOri).SearchForInitialization(F[0], F[1], prev, m12, window)
+    no, m12o = search_for_initialization(F[0].mvKeys, F[0].mDescriptors, F[1].mvKeys, F[1].mDescriptors, W, H,
+                                         prev_o, nnratio, checkOri, window)
+    assert n == no and np.array_equal(np.array(m12, np.int32), m12o)
+
+
+def test_match_batch_device_parity():
+    import torch
+
+    B, W, H = 8, 640, 480
+    frames = orb.synth_stream(W, H, stream=4, first=0, count=B)
+    ext = orb.ORBextractor(1000, 1.2, 8, orb.FAST_SCORE, 20, device=0, max_batch=B)
+    d = torch.from_numpy(frames).cuda()
+    kps, desc, counts = ext.extract_batch_device(d)
+    f1 = torch.arange(0, B - 1, dtype=torch.int32, device="cuda")
+    f2 = f1 + 1
+    m12, nm = orb.ORBmatcher(0.9, True).search_for_initialization_batch_device(kps, desc, counts, f1, f2, W, H, 100)
+    torch.cuda.synchronize()
+    kps_h, desc_h, cnt = kps.cpu().numpy(), desc.cpu().numpy(), counts.cpu().numpy()
+    m12, nm = m12.cpu().numpy(), nm.cpu().numpy()
+    for p in range(B - 1):
+        n1, n2 = cnt[p], cnt[p + 1]
+        k1 = orb.keypoints_from_bytes(kps_h[p], n1)
+        k2 = orb.keypoints_from_bytes(kps_h[p + 1], n2)
+        prev = np.ascontiguousarray(np.stack([k1["x"], k1["y"]], 1).astype(np.float32))
+        no, m12o = search_for_initialization(k1, desc_h[p, :n1], k2, desc_h[p + 1, :n2], W, H, prev, 0.9, True, 100)
+        assert nm[p] == no
+        assert np.array_equal(m12[p, :n1], m12o)
