@@ -1,0 +1,268 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json's metric: frames/s of ORB extract + match on 640x480 frames.
+
+A step = one pass of the hot path over one batch of B synthetic 640x480 frames resident in
+HBM: ORBextractor(1000, 1.2, 8, FAST, 20) on all B frames (orb_extract_batch_device), then
+ORBmatcher(0.9, true).SearchForInitialization(F_t, F_t+1, window 100) on the B-1
+consecutive pairs (orb_search_for_initialization_batch_device).  N GPUs run N independent
+replicas (frames shard one stream per GPU; no collectives on the data path); value is the
+whole-job frames/s = N * B * K / max-over-ranks(time of K steps).
+
+Also reported:
+  roofline      dominant kernel: algorithmic bytes per launch / mean launch duration, from
+                HIP events recorded around every kernel stage on its launch stream.
+  pipeline      whole-path algorithmic bytes (SURVEY.md §8d B_ext + B_match) / wall time.
+  cpu_baseline  the CPU oracle (C++ restatement, oracle/) on the host cores, rank 0 only,
+                on a bounded sample of the same frames.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md §Chip-level parameters)
+
+
+def level_sizes(W, H, nlevels=8, scale=1.2):
+    """(w_l, h_l) exactly as ComputePyramid (ORBextractor.cc:783-786)."""
+    inv = [np.float32(1.0)]
+    f = np.float32(np.float32(1.0) / np.float64(np.float32(scale)))
+    for _ in range(1, nlevels):
+        inv.append(np.float32(inv[-1] * f))
+    out = []
+    for s in inv:
+        out.append((int(np.rint(np.float64(np.float32(W) * s))), int(np.rint(np.float64(np.float32(H) * s)))))
+    return out
+
+
+def stage_bytes(W, H, n_kp, n_cand, n_pairs_kp0, B):
+    """Algorithmic HBM bytes per launch of each stage for a batch of B frames.
+
+    n_kp: total keypoints of the batch; n_cand: total FAST survivors; n_pairs_kp0: sum over
+    pairs of (n1_0 + n2_0) level-0 keypoints.  Definitions in DESIGN.md §Roofline.
+    """
+    lv = level_sizes(W, H)
+    pad = [(w + 32) * (h + 32) for w, h in lv]
+    px = [w * h for w, h in lv]
+    det = [max(w - 26, 0) * max(h - 26, 0) for w, h in lv]  # cell ROIs: detection area + 3 px halo
+    return {
+        "k_pyr0": B * (W * H + pad[0]),
+        "k_pyr_resize": B * sum(px[l - 1] + pad[l] for l in range(1, len(lv))) / (len(lv) - 1),  # per launch
+        "k_fast_cells": B * sum(det) + 4 * n_cand,
+        "k_select": 8 * n_cand + 4 * n_kp,
+        "k_orient_desc": n_kp * (4 + 43 * 43 + 60),
+    }
+
+
+def cpu_baseline(frames, nfeatures, threads, W, H):
+    """Oracle (test infrastructure, oracle/liborb_oracle.so) on a bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import ctypes
+
+    from oracle_lib import lib
+
+    L = lib()
+    fr = np.ascontiguousarray(frames)
+    k = ctypes.c_int64()
+    m = ctypes.c_int64()
+    L.oracle_bench(nfeatures, 1.2, 8, 20, fr[:8].ctypes.data_as(ctypes.c_void_p), min(8, len(fr)), W, H, W, W * H,
+                   threads, 1, ctypes.byref(k), ctypes.byref(m))  # warm-up
+    dt = L.oracle_bench(nfeatures, 1.2, 8, 20, fr.ctypes.data_as(ctypes.c_void_p), len(fr), W, H, W, W * H, threads,
+                        1, ctypes.byref(k), ctypes.byref(m))
+    if dt <= 0:
+        raise RuntimeError("oracle_bench failed")
+    return len(fr) / dt, dt, int(k.value), int(m.value)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256, help="frames per step per GPU")
+    ap.add_argument("--width", type=int, default=640)
+    ap.add_argument("--height", type=int, default=480)
+    ap.add_argument("--nfeatures", type=int, default=1000)
+    ap.add_argument("--cpu-frames", type=int, default=1024, help="CPU-baseline sample size (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = OMP_NUM_THREADS or os.cpu_count()")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import orbslam_jpminipc_amd as orb
+
+    W, H, B, NF = args.width, args.height, args.batch, args.nfeatures
+    frames = orb.synth_stream(W, H, stream=rank, first=0, count=B)
+    d_imgs = torch.from_numpy(frames).cuda()
+    ext = orb.ORBextractor(NF, 1.2, 8, orb.FAST_SCORE, 20, device=local, max_batch=B)
+    matcher = orb.ORBmatcher(0.9, True)
+    cap = ext.max_keypoints
+    d_kps = torch.empty((B, cap, 28), dtype=torch.uint8, device="cuda")
+    d_desc = torch.empty((B, cap, 32), dtype=torch.uint8, device="cuda")
+    d_cnt = torch.empty((B,), dtype=torch.int32, device="cuda")
+    f1 = torch.arange(0, B - 1, dtype=torch.int32, device="cuda")
+    f2 = f1 + 1
+    stream = torch.cuda.current_stream()
+    ev_m = []
+
+    def step(timed=False):
+        ext.extract_batch_device(d_imgs, d_kps, d_desc, d_cnt, stream=stream)
+        if timed:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+        m12, nm = matcher.search_for_initialization_batch_device(d_kps, d_desc, d_cnt, f1, f2, W, H, 100,
+                                                                 stream=stream)
+        if timed:
+            b.record(stream)
+            ev_m.append((a, b))
+        return nm
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ext.profile_enable(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        nm = step(timed=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    prof = ext.profile_read()
+    ext.profile_enable(False)
+    match_ms = sum(a.elapsed_time(b) for a, b in ev_m)
+    prof["k_match_init"] = (match_ms, len(ev_m))
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    tmax = float(t.item())
+
+    # workload statistics of the last step (identical every step: same frames)
+    cnt = d_cnt.cpu().numpy().astype(np.int64)
+    kps_h = d_kps.cpu().numpy()
+    oct0 = np.array([int((orb.keypoints_from_bytes(kps_h[b], cnt[b])["octave"] == 0).sum()) for b in range(B)])
+    n_kp = int(cnt.sum())
+    nm_h = nm.cpu().numpy()
+    n_cand = int(n_kp * 3)  # refined below from the FAST survivors when available
+    try:
+        import ctypes
+
+        lib = orb.hip_lib()
+        tot = 0
+        buf = np.zeros(4096, np.int32)
+        for b in range(B):
+            for l in range(8):
+                n = lib.orb_debug_cell_counts(ext._h, b, l, buf.ctypes.data_as(ctypes.c_void_p), 4096)
+                tot += int(buf[:n].sum())
+        n_cand = tot
+    except Exception:
+        pass
+    pairs_kp0 = int(sum(oct0[p] + oct0[p + 1] for p in range(B - 1)))
+    sb = stage_bytes(W, H, n_kp, n_cand, pairs_kp0, B)
+    lv = level_sizes(W, H)
+    px = [w * h for w, h in lv]
+    b_ext = B * (sum(px) + sum(px[1:])) + 60 * n_kp
+    b_match = 32 * pairs_kp0 + 20 * int(sum(cnt[:-1]))
+    sb["k_match_init"] = b_match
+    stages = {}
+    for name, (ms, launches) in prof.items():
+        if launches == 0:
+            continue
+        per_launch_ms = ms / launches
+        nbytes = sb.get(name, 0)
+        stages[name] = {
+            "ms_per_launch": per_launch_ms,
+            "launches": launches,
+            "bytes_per_launch": nbytes,
+            "GBps": nbytes / (per_launch_ms * 1e-3) / 1e9 if per_launch_ms > 0 else None,
+        }
+    # the resize stage launches one kernel per level: report per-kernel-launch numbers
+    if "k_pyr_resize" in stages:
+        s = stages["k_pyr_resize"]
+        s["launches"] *= 7
+        s["ms_per_launch"] /= 7
+        s["GBps"] = s["bytes_per_launch"] / (s["ms_per_launch"] * 1e-3) / 1e9
+    dom = max(stages, key=lambda k: stages[k]["ms_per_launch"] * stages[k]["launches"])
+    ds = stages[dom]
+    per_step_s = tmax / args.steps
+
+    value = world * B * args.steps / tmax
+    result = {
+        "metric": "frames/sec ORB extract+match, 640x480 8-level 1000 kp; HBM GB/s vs peak",
+        "value": value,
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": per_step_s * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (csrc/synth.c: rectangles+discs+noise, consecutive frames shifted)",
+        "config": {
+            "workload": f"{W}x{H} frames, ORBextractor({NF},1.2,8,FAST,20) + SearchForInitialization(t,t+1) "
+                        f"nnratio 0.9 checkOri window 100 (BASELINE.json configs[1]+[2])",
+            "batch_per_gpu": B,
+            "pairs_per_gpu": B - 1,
+            "parallelism": f"replicas x{world} (one stream per GPU, no collectives)",
+        },
+        "roofline": {
+            "kernel": dom,
+            "bound": "hbm",
+            "achieved": ds["GBps"],
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": ds["GBps"] / HBM_PEAK_GBS if ds["GBps"] else None,
+            "traffic": None,
+        },
+        "pipeline": {
+            "algorithmic_bytes_per_step": b_ext + b_match,
+            "GBps": (b_ext + b_match) / per_step_s / 1e9,
+            "frac": (b_ext + b_match) / per_step_s / 1e9 / HBM_PEAK_GBS,
+        },
+        "stages": stages,
+        "workload_stats": {"keypoints_per_frame": n_kp / B, "fast_survivors_per_frame": n_cand / B,
+                           "matches_per_pair": float(nm_h.mean())},
+    }
+    if rank == 0 and world == 1 and args.cpu_frames > 0:
+        threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or os.cpu_count())
+        ncpu = args.cpu_frames
+        cpu_frames = orb.synth_stream(W, H, stream=0, first=0, count=ncpu)
+        fps, dt, _, _ = cpu_baseline(cpu_frames, NF, threads, W, H)
+        result["cpu_baseline"] = {
+            "value": fps,
+            "unit": "frames/s",
+            "cores": threads,
+            "kind": "port",
+            "sample": f"{ncpu} frames extract + {ncpu - 1} consecutive-pair SearchForInitialization, "
+                      f"{dt:.2f} s wall on {threads} threads (C++ restatement oracle, -O3)",
+        }
+    if rank == 0:
+        print(json.dumps(result))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

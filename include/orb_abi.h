@@ -130,6 +130,16 @@ int orb_search_for_initialization_batch_device(const orb_keypoint_t* d_kps, cons
                                                int check_ori, int window, float* d_prev_xy, int32_t* d_matches12,
                                                int32_t* d_nmatches, void* stream);
 
+/* ---- measurement ------------------------------------------------------------------- */
+/* Per-stage HIP-event timing of the extraction kernels: when enabled, every
+ * orb_extract_batch_device records an event pair around each stage on its launch stream.
+ * orb_profile_read synchronises and returns cumulative milliseconds and launch counts per
+ * stage (stage names via orb_profile_stage_name); the return value is the stage count.
+ * Enabling (or re-enabling) resets the counters. */
+int orb_profile_enable(orb_extractor_t* h, int enable);
+int orb_profile_read(orb_extractor_t* h, double* stage_ms, int64_t* stage_launches, int nstages);
+const char* orb_profile_stage_name(int i);
+
 /* ---- test hooks (no device work unless stated) ------------------------------------- */
 /* Host instantiation of the kernels' libstdc++ nth_element replay on packed u32 elements
  * (score in bits 24..31), for CPU unit tests against std::nth_element. */

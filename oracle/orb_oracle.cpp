@@ -1156,7 +1156,7 @@ double oracle_bench(int nfeatures, float scale_factor, int nlevels, int fast_th,
     if (threads <= 0) threads = 1;
     std::vector<orb_keypoint_t> kps((size_t)B * nfeatures);
     std::vector<uint8_t> desc((size_t)B * nfeatures * 32);
-    std::vector<int> counts(B, 0), nm(B / 2, 0), status(threads, 0);
+    std::vector<int> counts(B, 0), nm(std::max(B - 1, 1), 0), status(threads, 0);
     orb_frame_bounds_t bounds{0, w, 0, hgt};
     auto t0 = std::chrono::steady_clock::now();
     std::vector<std::thread> pool;
@@ -1176,8 +1176,8 @@ double oracle_bench(int nfeatures, float scale_factor, int nlevels, int fast_th,
             pool.emplace_back([&, t]() {
                 std::vector<float> prev(2 * (size_t)nfeatures);
                 std::vector<int32_t> m12(nfeatures);
-                for (int p = t; p < B / 2; p += threads) {
-                    const int f1 = 2 * p, f2 = 2 * p + 1;
+                for (int p = t; p < B - 1; p += threads) {
+                    const int f1 = p, f2 = p + 1;
                     for (int i = 0; i < counts[f1]; ++i) {
                         prev[2 * i] = kps[(size_t)f1 * nfeatures + i].x;
                         prev[2 * i + 1] = kps[(size_t)f1 * nfeatures + i].y;

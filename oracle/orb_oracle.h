@@ -72,7 +72,7 @@ int oracle_search_by_bow_kf_kf(const orb_keypoint_t* kps1, const uint8_t* desc1,
 
 /* CPU baseline: extract B frames (frame k at imgs + k*pitch) with `threads` workers (one
  * extractor per worker, frames round-robin) and, if match != 0, SearchForInitialization on
- * consecutive pairs (2k, 2k+1) with window 100.  Returns wall seconds (< 0 on error). */
+ * consecutive pairs (t, t+1) with window 100.  Returns wall seconds (< 0 on error). */
 double oracle_bench(int nfeatures, float scale_factor, int nlevels, int fast_th, const uint8_t* imgs, int B, int w,
                     int hgt, int stride, int64_t pitch, int threads, int match, int64_t* total_kps,
                     int64_t* total_matches);

@@ -83,6 +83,9 @@ HIP_SIGNATURES = {
         _i,
         [_vp, _vp, _vp, _i, _i, _vp, _vp, FrameBounds, _f, _i, _i, _vp, _vp, _vp, _vp],
     ),
+    "orb_profile_enable": (_i, [_vp, _i]),
+    "orb_profile_read": (_i, [_vp, _vp, _vp, _i]),
+    "orb_profile_stage_name": (ctypes.c_char_p, [_i]),
     "orb_debug_nth_element_u32": (_i, [_vp, _i, _i]),
     "orb_debug_level_image": (_i, [_vp, _i, _i, _vp, ctypes.POINTER(_i), ctypes.POINTER(_i)]),
     "orb_debug_cell_counts": (_i, [_vp, _i, _i, _vp, _i]),
@@ -92,10 +95,25 @@ _hip = None
 _synth = None
 
 
+def _bind_torch_runtime() -> None:
+    """Import torch before dlopen-ing liborb_hip.so.
+
+    PyTorch-ROCm ships its own libamdhip64 (same SONAME, libamdhip64.so.7).  Loading it
+    first makes the dynamic linker bind liborb_hip.so to that copy, so the process has ONE
+    HIP runtime and torch-allocated device memory / streams are valid in our kernels.  (If
+    liborb_hip.so were loaded first, torch would start a second runtime and see no GPU.)
+    """
+    try:
+        import torch  # noqa: F401
+    except Exception:  # torch absent: the C ABI works standalone on /opt/rocm's runtime
+        pass
+
+
 def hip_lib() -> ctypes.CDLL:
     """Load liborb_hip.so (fails loudly: there is no CPU fallback)."""
     global _hip
     if _hip is None:
+        _bind_torch_runtime()
         if not HIP_LIB_PATH.exists():
             raise NativeLibraryError(
                 f"{HIP_LIB_PATH} is missing; run `python -c 'import __graft_entry__ as g; g.build()'`"

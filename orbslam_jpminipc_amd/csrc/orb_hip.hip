@@ -766,11 +766,26 @@ struct orb_extractor {
     int* d_lvlCount = nullptr;
     int* d_rtab = nullptr;
     CellGeom* d_cells = nullptr;
+    // per-stage HIP-event timing (orb_profile_*): stage k brackets its kernel(s) on the launch stream
+    static constexpr int kStages = 5;
+    bool prof = false;
+    std::vector<hipEvent_t> evPool;  // 2 per stage per launch, recycled after each read
+    std::vector<std::pair<int, int>> evPending;  // (stage, index of the start event)
+    double stageMs[kStages] = {};
+    long long stageLaunches[kStages] = {};
+    int evNext = 0;
     // staging for host-buffer entry points
     uint8_t* d_img = nullptr;
     orb_keypoint_t* d_kps = nullptr;
     uint8_t* d_desc = nullptr;
     int* d_counts = nullptr;
+
+    void free_events() {
+        for (auto e : evPool) hipEventDestroy(e);
+        evPool.clear();
+        evPending.clear();
+        evNext = 0;
+    }
 
     void free_ws() {
         hipFree(d_pyr);
@@ -1004,24 +1019,71 @@ struct orb_extractor {
         return ORB_OK;
     }
 
+    hipEvent_t next_event() {
+        if (evNext == (int)evPool.size()) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+            evPool.push_back(e);
+        }
+        return evPool[evNext++];
+    }
+    void stage_begin(int stage, hipStream_t st) {
+        if (!prof) return;
+        int i = evNext;
+        hipEvent_t a = next_event(), b = next_event();
+        if (!a || !b) return;
+        hipEventRecord(a, st);
+        evPending.push_back({stage, i});
+    }
+    void stage_end(hipStream_t st) {
+        if (!prof || evPending.empty()) return;
+        hipEventRecord(evPool[evPending.back().second + 1], st);
+    }
+    int profile_collect() {
+        for (auto& pe : evPending) {
+            HIP_TRY(hipEventSynchronize(evPool[pe.second + 1]));
+            float ms = 0.f;
+            HIP_TRY(hipEventElapsedTime(&ms, evPool[pe.second], evPool[pe.second + 1]));
+            stageMs[pe.first] += ms;
+            stageLaunches[pe.first] += 1;
+        }
+        evPending.clear();
+        evNext = 0;
+        return ORB_OK;
+    }
+
     int launch(int B, const uint8_t* d_imgs, int stride, long long fpitch, orb_keypoint_t* kps, uint8_t* desc,
                int* counts, hipStream_t st) {
+        if (prof && evNext > 4096) {  // bound the pool between reads
+            int r = profile_collect();
+            if (r) return r;
+        }
+        stage_begin(0, st);
         {
             const LevelGeom& lg = g.lv[0];
             dim3 grid((lg.pitch / 4 + 255) / 256, lg.ph, B);
             hipLaunchKernelGGL(k_pyr0, grid, dim3(256), 0, st, d_imgs, stride, fpitch, d_pyr, g);
         }
+        stage_end(st);
+        stage_begin(1, st);
         for (int l = 1; l < nlevels; ++l) {
             const LevelGeom& lg = g.lv[l];
             dim3 grid((lg.pitch / 4 + 255) / 256, lg.ph, B);
             hipLaunchKernelGGL(k_pyr_resize, grid, dim3(256), 0, st, d_pyr, d_rtab, g, l);
         }
+        stage_end(st);
+        stage_begin(2, st);
         hipLaunchKernelGGL(k_fast_cells, dim3(g.nCells, B), dim3(256), cellLds, st, d_pyr, g, d_cells, d_cand,
                            d_cellCount);
+        stage_end(st);
+        stage_begin(3, st);
         hipLaunchKernelGGL(k_select, dim3(nlevels, B), dim3(64), 0, st, d_cand, d_cellCount, g, d_cells, d_lvl,
                            d_lvlCount);
+        stage_end(st);
+        stage_begin(4, st);
         dim3 gd((std::max(kpCap, 1) + 3) / 4, B);
         hipLaunchKernelGGL(k_orient_desc, gd, dim3(256), 0, st, d_pyr, g, d_lvl, d_lvlCount, kps, desc, counts);
+        stage_end(st);
         HIP_TRY(hipGetLastError());
         return ORB_OK;
     }
@@ -1084,6 +1146,7 @@ int orb_extractor_destroy(orb_extractor_t* h) {
     hipSetDevice(h->device);
     hipStreamSynchronize(h->stream);
     h->free_ws();
+    h->free_events();
     hipStreamDestroy(h->stream);
     delete h;
     return ORB_OK;
@@ -1266,6 +1329,37 @@ int orb_search_for_initialization(const orb_keypoint_t* kps1, const uint8_t* des
     if (e != hipSuccess) return set_err(ORB_EDEVICE, std::string("match: ") + hipGetErrorString(e));
     *n_matches = nm;
     return ORB_OK;
+}
+
+static const char* kStageNames[] = {"k_pyr0", "k_pyr_resize", "k_fast_cells", "k_select", "k_orient_desc"};
+
+int orb_profile_enable(orb_extractor_t* h, int enable) {
+    if (!h) return set_err(ORB_EINVAL, "bad handle");
+    HIP_TRY(hipSetDevice(h->device));
+    int r = h->profile_collect();
+    if (r) return r;
+    h->prof = enable != 0;
+    for (int k = 0; k < orb_extractor::kStages; ++k) {
+        h->stageMs[k] = 0;
+        h->stageLaunches[k] = 0;
+    }
+    return ORB_OK;
+}
+
+int orb_profile_read(orb_extractor_t* h, double* stage_ms, int64_t* stage_launches, int nstages) {
+    if (!h || nstages < 0) return set_err(ORB_EINVAL, "bad arguments");
+    HIP_TRY(hipSetDevice(h->device));
+    int r = h->profile_collect();
+    if (r) return r;
+    for (int k = 0; k < nstages && k < orb_extractor::kStages; ++k) {
+        if (stage_ms) stage_ms[k] = h->stageMs[k];
+        if (stage_launches) stage_launches[k] = h->stageLaunches[k];
+    }
+    return orb_extractor::kStages;
+}
+
+const char* orb_profile_stage_name(int i) {
+    return (i >= 0 && i < orb_extractor::kStages) ? kStageNames[i] : "";
 }
 
 // ---- debug / test hooks (no device work) ------------------------------------------------

@@ -123,6 +123,19 @@ class ORBextractor:
         return d_kps, d_desc, d_counts
 
 
+    # ---- measurement ----------------------------------------------------------------------
+    def profile_enable(self, enable: bool = True) -> None:
+        """Record a HIP-event pair around every kernel stage of extract_batch_device."""
+        check(self._lib.orb_profile_enable(self._h, int(enable)))
+
+    def profile_read(self) -> dict:
+        """{stage_name: (cumulative_ms, launches)} since profile_enable (synchronises)."""
+        ms = np.zeros(16, np.float64)
+        n = np.zeros(16, np.int64)
+        k = check(self._lib.orb_profile_read(self._h, ptr(ms), ptr(n), 16))
+        return {self._lib.orb_profile_stage_name(i).decode(): (float(ms[i]), int(n[i])) for i in range(k)}
+
+
 def keypoints_from_bytes(raw: np.ndarray, n: int) -> np.ndarray:
     """View n records of a (cap, 28) uint8 buffer as KEYPOINT_DTYPE."""
     return np.ascontiguousarray(raw[:n]).view(KEYPOINT_DTYPE).reshape(-1)
