@@ -25,7 +25,6 @@ import time
 
 import numpy as np
 import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -60,7 +59,8 @@ def stage_bytes(W, H, n_kp, n_cand, n_pairs_kp0, B):
         "k_pyr_resize": B * sum(px[l - 1] + pad[l] for l in range(1, len(lv))) / (len(lv) - 1),  # per launch
         "k_fast_cells": B * sum(det) + 4 * n_cand,
         "k_select": 8 * n_cand + 4 * n_kp,
-        "k_orient_desc": n_kp * (4 + 43 * 43 + 60),
+        "k_blur": B * sum((w + 12) * (h + 12) + (w + 6) * (h + 6) for w, h in lv),
+        "k_orient_desc": n_kp * (4 + 31 * 31 + 512 + 60),
     }
 
 
@@ -97,14 +97,12 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = OMP_NUM_THREADS or os.cpu_count()")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-
     import orbslam_jpminipc_amd as orb
+    from orbslam_jpminipc_amd import replicas
+
+    info = replicas.init_from_env("nccl")
+    world, rank, local = info.world, info.rank, info.local_rank
+    torch.cuda.set_device(local)
 
     W, H, B, NF = args.width, args.height, args.batch, args.nfeatures
     frames = orb.synth_stream(W, H, stream=rank, first=0, count=B)
@@ -136,15 +134,13 @@ def main():
         step()
     torch.cuda.synchronize()
     ext.profile_enable(True)
-    if world > 1:
-        dist.barrier()
+    replicas.barrier(info)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         nm = step(timed=True)
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    replicas.barrier(info)
     t1 = time.perf_counter()
     elapsed = t1 - t0
     prof = ext.profile_read()
@@ -152,10 +148,7 @@ def main():
     match_ms = sum(a.elapsed_time(b) for a, b in ev_m)
     prof["k_match_init"] = (match_ms, len(ev_m))
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    tmax = float(t.item())
+    tmax = replicas.max_over_ranks(elapsed, info)
 
     # workload statistics of the last step (identical every step: same frames)
     cnt = d_cnt.cpu().numpy().astype(np.int64)
@@ -206,7 +199,7 @@ def main():
     ds = stages[dom]
     per_step_s = tmax / args.steps
 
-    value = world * B * args.steps / tmax
+    value = replicas.whole_job_rate(B * args.steps, world, tmax)
     result = {
         "metric": "frames/sec ORB extract+match, 640x480 8-level 1000 kp; HBM GB/s vs peak",
         "value": value,
@@ -260,8 +253,7 @@ def main():
         }
     if rank == 0:
         print(json.dumps(result))
-    if world > 1:
-        dist.destroy_process_group()
+    replicas.shutdown(info)
 
 
 if __name__ == "__main__":

@@ -971,6 +971,36 @@ void oracle_nth_element_greater(const float* keys, int32_t* idx, int n, int nth)
 
 void oracle_gaussian_taps(int* taps7) { gaussian_taps(taps7); }
 
+int oracle_rot_bin(float a1, float a2) { return rot_bin(a1, a2); }
+
+int oracle_resize(const uint8_t* src, int sstep, int sw, int sh, uint8_t* dst, int dstep, int dw, int dh) {
+    return resize_linear_8u(src, sstep, sw, sh, dst, dstep, dw, dh);
+}
+
+/* GaussianBlur(7x7, sigma 2) of a (w+32) x (h+32) padded image's ROI (out: w x h). */
+int oracle_blur_padded(const uint8_t* padded, int w, int hgt, uint8_t* out) {
+    Level L;
+    L.alloc(w, hgt);
+    std::memcpy(L.buf.data(), padded, L.buf.size());
+    std::vector<uint8_t> o;
+    gaussian_blur_level(L, o);
+    std::memcpy(out, o.data(), o.size());
+    return ORB_OK;
+}
+
+/* FAST on a region (cv::FAST(img, kps, t, true)); out: n x 3 int (x, y, score). */
+int oracle_fast(const uint8_t* img, int step, int cols, int rows, int threshold, int32_t* out, int cap) {
+    std::vector<KP> k;
+    fast16(img, step, cols, rows, threshold, k);
+    if ((int)k.size() > cap) return ORB_ERANGE;
+    for (size_t i = 0; i < k.size(); ++i) {
+        out[3 * i] = (int)k[i].x;
+        out[3 * i + 1] = (int)k[i].y;
+        out[3 * i + 2] = (int)k[i].response;
+    }
+    return (int)k.size();
+}
+
 int oracle_features_in_area(const orb_keypoint_t* kps, int n, orb_frame_bounds_t bounds, float x, float y, float r,
                             int min_level, int max_level, int32_t* out, int cap) {
     OFrame F(kps, nullptr, n, bounds);

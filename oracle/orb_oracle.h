@@ -43,6 +43,14 @@ int oracle_descriptor_distance(const uint8_t* a, const uint8_t* b);
 void oracle_nth_element_greater(const float* keys, int32_t* idx, int n, int nth);
 /* OpenCV 2.4 getGaussianKernel(7, 2, CV_32F) * 256 -> int (the blur's fixed-point taps). */
 void oracle_gaussian_taps(int* taps7);
+/* ORBmatcher rotation-histogram bin of (a1 - a2) (ORBmatcher.cc:668-673). */
+int oracle_rot_bin(float a1, float a2);
+/* cv::resize(INTER_LINEAR) 8U restatement. */
+int oracle_resize(const uint8_t* src, int sstep, int sw, int sh, uint8_t* dst, int dstep, int dw, int dh);
+/* GaussianBlur(7x7, sigma 2) of the ROI of a (w+32) x (h+32) padded image (out: w x h). */
+int oracle_blur_padded(const uint8_t* padded, int w, int hgt, uint8_t* out);
+/* cv::FAST(img, kps, t, nonmax=true) on a region; out n x 3 (x, y, score); returns n. */
+int oracle_fast(const uint8_t* img, int step, int cols, int rows, int threshold, int32_t* out, int cap);
 
 int oracle_search_for_initialization(const orb_keypoint_t* kps1, const uint8_t* desc1, int n1,
                                      const orb_keypoint_t* kps2, const uint8_t* desc2, int n2,

@@ -100,9 +100,9 @@ __constant__ signed char c_pattern[1024];
 __global__ void __launch_bounds__(256) k_pyr0(const uint8_t* __restrict__ imgs, int stride, long long fpitch,
                                               uint8_t* __restrict__ pyr, Geom g) {
     const LevelGeom& lg = g.lv[0];
-    const int b = blockIdx.z, py = blockIdx.y;
-    const int x4 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
-    if (x4 >= lg.pitch) return;
+    const int b = blockIdx.z, py = blockIdx.y * 4 + threadIdx.y;
+    const int x4 = (blockIdx.x * 64 + threadIdx.x) * 4;
+    if (x4 >= lg.pitch || py >= lg.ph) return;
     const uint8_t* src = imgs + (long long)b * fpitch + (long long)reflect101(py - EDGE, lg.h) * stride;
     uint32_t word = 0;
 #pragma unroll
@@ -118,93 +118,199 @@ __global__ void __launch_bounds__(256) k_pyr0(const uint8_t* __restrict__ imgs, 
 // Level l >= 1: cv::resize(level l-1, (w_l, h_l), INTER_LINEAR) for 8U:
 // fixed-point HResizeLinear rows; vertical SSE2 body (VResizeLinearVec_32s8u) for x < xs,
 // scalar FixedPtCast<int,uchar,22> tail; then copyMakeBorder(REFLECT_101 | ISOLATED), fused
-// by evaluating the resize at the reflected coordinate of every padded pixel.
+// by evaluating the resize at the reflected coordinate of every padded pixel.  A thread owns
+// 4 padded columns (coefficients kept in registers) and walks PYR_RW padded rows.
+#define PYR_RW 16
 __global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, const int* __restrict__ rtab, Geom g,
                                                     int l) {
     const LevelGeom& lg = g.lv[l];
     const LevelGeom& ls = g.lv[l - 1];
-    const int b = blockIdx.z, py = blockIdx.y;
-    const int x4 = (blockIdx.x * blockDim.x + threadIdx.x) * 4;
-    if (x4 >= lg.pitch) return;
+    const int b = blockIdx.z;
+    const int x4 = (blockIdx.x * 64 + threadIdx.x) * 4;
+    const int py0 = (blockIdx.y * 4 + threadIdx.y) * PYR_RW;
+    if (x4 >= lg.pitch || py0 >= lg.ph) return;
     const int* xofs = rtab + lg.rtab;
     const int* alpha = xofs + lg.w;
     const int* yofs = alpha + lg.w;
     const int* beta = yofs + lg.h;
-    const int ly = reflect101(py - EDGE, lg.h);
-    const int sy = yofs[ly];
-    const int r0 = min(max(sy, 0), ls.h - 1), r1 = min(max(sy + 1, 0), ls.h - 1);
-    const int bb = beta[ly];
-    const int b0 = (short)(bb & 0xFFFF), b1 = (short)(bb >> 16);
-    const uint8_t* S = pyr + ls.base + (long long)b * ls.fstride + (long long)EDGE * ls.pitch + EDGE;
-    const uint8_t* S0 = S + (long long)r0 * ls.pitch;
-    const uint8_t* S1 = S + (long long)r1 * ls.pitch;
-    uint32_t word = 0;
+    int sx[4], a0[4], a1[4];
+    bool live[4], simd[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        int px = x4 + i;
-        uint32_t v = 0;
-        if (px < lg.w + 2 * EDGE) {
-            int lx = reflect101(px - EDGE, lg.w);
-            int sx = xofs[lx];
-            int H0, H1;
-            if (lx < lg.xmax) {
-                int aa = alpha[lx];
-                int a0 = (short)(aa & 0xFFFF), a1 = (short)(aa >> 16);
-                H0 = S0[sx] * a0 + S0[sx + 1] * a1;
-                H1 = S1[sx] * a0 + S1[sx + 1] * a1;
-            } else {
-                H0 = S0[sx] * 2048;
-                H1 = S1[sx] * 2048;
-            }
+        const int px = x4 + i;
+        live[i] = px < lg.w + 2 * EDGE;
+        const int lx = reflect101(min(px, lg.w + 2 * EDGE - 1) - EDGE, lg.w);
+        sx[i] = xofs[lx];
+        if (lx < lg.xmax) {
+            const int aa = alpha[lx];
+            a0[i] = (short)(aa & 0xFFFF);
+            a1[i] = (short)(aa >> 16);
+        } else {  // HResizeLinear tail: S[sx] * ONE
+            a0[i] = 2048;
+            a1[i] = 0;
+        }
+        simd[i] = lx < lg.xs_resize;
+    }
+    const uint8_t* S = pyr + ls.base + (long long)b * ls.fstride + (long long)EDGE * ls.pitch + EDGE;
+    uint8_t* D = pyr + lg.base + (long long)b * lg.fstride + x4;
+    const int py1 = min(py0 + PYR_RW, lg.ph);
+    for (int py = py0; py < py1; ++py) {
+        const int ly = reflect101(py - EDGE, lg.h);
+        const int sy = yofs[ly];
+        const int bb = beta[ly];
+        const int b0 = (short)(bb & 0xFFFF), b1 = (short)(bb >> 16);
+        const uint8_t* S0 = S + (long long)min(max(sy, 0), ls.h - 1) * ls.pitch;
+        const uint8_t* S1 = S + (long long)min(max(sy + 1, 0), ls.h - 1) * ls.pitch;
+        uint32_t word = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            // a1 == 0 on the tail columns, where sx + 1 may be past the row: index sx instead
+            const int sx1 = a1[i] ? sx[i] + 1 : sx[i];
+            const int H0 = S0[sx[i]] * a0[i] + S0[sx1] * a1[i];
+            const int H1 = S1[sx[i]] * a0[i] + S1[sx1] * a1[i];
             int r;
-            if (lx < lg.xs_resize) {
-                int h0 = min(max(H0 >> 4, -32768), 32767), h1 = min(max(H1 >> 4, -32768), 32767);
-                int s = min(max(((h0 * b0) >> 16) + ((h1 * b1) >> 16), -32768), 32767);
-                s = min(max(s + 2, -32768), 32767);
-                r = s >> 2;
+            if (simd[i]) {
+                const int h0 = min(max(H0 >> 4, -32768), 32767), h1 = min(max(H1 >> 4, -32768), 32767);
+                int sm = min(max(((h0 * b0) >> 16) + ((h1 * b1) >> 16), -32768), 32767);
+                sm = min(max(sm + 2, -32768), 32767);
+                r = sm >> 2;
             } else {
                 r = (H0 * b0 + H1 * b1 + (1 << 21)) >> 22;
             }
-            v = (uint32_t)min(max(r, 0), 255);
+            word |= (live[i] ? (uint32_t)min(max(r, 0), 255) : 0u) << (8 * i);
         }
-        word |= v << (8 * i);
+        *(uint32_t*)(D + (long long)py * lg.pitch) = word;
     }
-    *(uint32_t*)(pyr + lg.base + (long long)b * lg.fstride + (long long)py * lg.pitch + x4) = word;
+}
+
+// ---- global -> LDS staging --------------------------------------------------------------
+// Copy `rows` rows of `words` dwords (global row stride gsw words, LDS row stride lsw words)
+// with 256 threads: waves take rows, lanes take words, and every thread issues up to 8
+// independent loads before its LDS stores, so a workgroup pays a few memory latencies
+// instead of one per row.  Words at or beyond `wlimit` in a row are not read (stay 0).
+__device__ __forceinline__ void stage_rows_to_lds(uint32_t* __restrict__ dst, int lsw,
+                                                  const uint32_t* __restrict__ src, long long gsw, int rows,
+                                                  int words, int wlimit, int wave, int lane) {
+    for (int wx0 = 0; wx0 < words; wx0 += 64) {
+        const int wx = wx0 + lane;
+        const bool colok = wx < words;
+        const bool inb = wx < wlimit;
+        for (int r0 = wave; r0 < rows; r0 += 32) {
+            uint32_t v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int r = r0 + 4 * k;
+                v[k] = (colok && inb && r < rows) ? src[(long long)r * gsw + wx] : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int r = r0 + 4 * k;
+                if (colok && r < rows) dst[r * lsw + wx] = v[k];
+            }
+        }
+    }
 }
 
 // ---- FAST per cell ----------------------------------------------------------------------
-// One workgroup per (cell, frame).  The cell ROI (cell + 3 px on each side) is staged in
-// LDS; S(p) is computed for the detection region [3, hx-3) x [3, hy-3); non-max suppression
-// is evaluated with out-of-region neighbours = 0, exactly as cv::FAST sees a cell-sized Mat.
-// If the cell yields <= 3 corners at fastTh it is re-run at threshold 7 (ORBextractor.cc:609-614).
-// Survivors are written in raster order as (score << 24) | (y << 12) | x, level coordinates.
-__device__ __forceinline__ int nms_keep(const uint8_t* Sb, int dw, int dh, int xx, int yy, int t) {
-    int s = Sb[yy * dw + xx];
-    if (s <= t) return 0;
-    int sc = s - 1;
+// One workgroup (4 waves) per (cell, frame); the cell ROI (cell + 3 px each side) is staged
+// in LDS.  For threshold t = fastTh (and again at t = 7 when that finds <= 3 corners,
+// ORBextractor.cc:609-614):
+//   detect  compass pre-filter (a 9-arc always covers two adjacent points of {0,4,8,12},
+//           the SSE2 pre-test of cv::FAST), full 16-point 9-arc test only in wave segments
+//           where some lane passed it; corners are queued in LDS
+//   score   exact S (cornerScore<16> + 1) for the queued corners only
+//   nms     3x3 non-max suppression around each queued corner; neighbours outside the
+//           detection region, and non-corners, score 0 — cv::FAST on a cell-sized Mat
+// then the survivors are compacted in raster order as (score << 24) | (y << 12) | x.
+#define FAST_LCAP 2048  // corners queued for scoring
+#define FAST_QCAP 4096  // pre-filter survivors queued for the full test
+
+// cv::FAST corner test at threshold t: >= 9 contiguous circle pixels all > v+t or all < v-t.
+__device__ __forceinline__ bool fast_is_corner(const uint8_t* p, int TP, int t) {
+    const int v = p[0], hi = v + t, lo = v - t;
+    int c16[16];
+    c16[0] = p[3 * TP];
+    c16[1] = p[3 * TP + 1];
+    c16[2] = p[2 * TP + 2];
+    c16[3] = p[TP + 3];
+    c16[4] = p[3];
+    c16[5] = p[-TP + 3];
+    c16[6] = p[-2 * TP + 2];
+    c16[7] = p[-3 * TP + 1];
+    c16[8] = p[-3 * TP];
+    c16[9] = p[-3 * TP - 1];
+    c16[10] = p[-2 * TP - 2];
+    c16[11] = p[-TP - 3];
+    c16[12] = p[-3];
+    c16[13] = p[TP - 3];
+    c16[14] = p[2 * TP - 2];
+    c16[15] = p[3 * TP - 1];
+    uint32_t bri = 0, drk = 0;
 #pragma unroll
-    for (int dy = -1; dy <= 1; ++dy)
+    for (int k = 0; k < 16; ++k) {
+        bri |= (uint32_t)(c16[k] > hi) << k;
+        drk |= (uint32_t)(c16[k] < lo) << k;
+    }
+    auto has9 = [](uint32_t m) {
+        uint32_t m32 = m | (m << 16);
+        uint32_t a2 = m32 & (m32 >> 1);
+        uint32_t a4 = a2 & (a2 >> 2);
+        uint32_t a8 = a4 & (a4 >> 4);
+        return (a8 & (m32 >> 8) & 0xFFFFu) != 0;
+    };
+    return has9(bri) || has9(drk);
+}
+
+__device__ __forceinline__ int fast_exact_strength(const uint8_t* p, int TP) {
+    int c[16];
+    c[0] = p[3 * TP];
+    c[1] = p[3 * TP + 1];
+    c[2] = p[2 * TP + 2];
+    c[3] = p[TP + 3];
+    c[4] = p[3];
+    c[5] = p[-TP + 3];
+    c[6] = p[-2 * TP + 2];
+    c[7] = p[-3 * TP + 1];
+    c[8] = p[-3 * TP];
+    c[9] = p[-3 * TP - 1];
+    c[10] = p[-2 * TP - 2];
+    c[11] = p[-TP - 3];
+    c[12] = p[-3];
+    c[13] = p[TP - 3];
+    c[14] = p[2 * TP - 2];
+    c[15] = p[3 * TP - 1];
+    const int v = p[0];
+    // A = max over arcs of min(v - c), B = max over arcs of min(c - v): sliding minima by
+    // doubling on (v - c, c - v) pairs
+    int a[24], bq[24];
 #pragma unroll
-        for (int dx = -1; dx <= 1; ++dx) {
-            if (dx == 0 && dy == 0) continue;
-            int nx = xx + dx, ny = yy + dy;
-            int ns = 0;
-            if (nx >= 0 && nx < dw && ny >= 0 && ny < dh) {
-                int v = Sb[ny * dw + nx];
-                ns = v > t ? v - 1 : 0;
-            }
-            if (!(sc > ns)) return 0;
-        }
-    return 1;
+    for (int k = 0; k < 24; ++k) {
+        a[k] = min(v - c[k & 15], v - c[(k + 1) & 15]);
+        bq[k] = min(c[k & 15] - v, c[(k + 1) & 15] - v);
+    }
+#pragma unroll
+    for (int k = 0; k < 22; ++k) {
+        a[k] = min(a[k], a[k + 2]);
+        bq[k] = min(bq[k], bq[k + 2]);
+    }
+    int A = -1000, B = -1000;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int ma = min(min(a[k], a[k + 4]), v - c[(k + 8) & 15]);
+        const int mb = min(min(bq[k], bq[k + 4]), c[(k + 8) & 15] - v);
+        A = max(A, ma);
+        B = max(B, mb);
+    }
+    return max(A, B);
 }
 
 __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ pyr, Geom g,
                                                     const CellGeom* __restrict__ cells, uint32_t* __restrict__ cand,
                                                     int* __restrict__ cellCount) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    __shared__ int s_cnt[256];
-    __shared__ int s_total;
+    __shared__ int s_nL, s_nQ, s_total;
     const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
     const CellGeom cg = cells[c];
     int* outCount = cellCount + (long long)b * g.nCells + c;
     const int dw = cg.hx - 6, dh = cg.hy - 6;
@@ -215,99 +321,174 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
     const LevelGeom& lg = g.lv[cg.level];
     const uint8_t* roi =
         pyr + lg.base + (long long)b * lg.fstride + (long long)(EDGE + cg.y0) * lg.pitch + EDGE + cg.x0;
-    const int tp = (cg.hx + 3) & ~3;
-    uint8_t* tile = smem;
-    uint8_t* Sb = smem + tp * cg.hy;
-    for (int i = tid; i < cg.hx * cg.hy; i += 256) {
-        int yy = i / cg.hx, xx = i - yy * cg.hx;
-        tile[yy * tp + xx] = roi[(long long)yy * lg.pitch + xx];
-    }
-    __syncthreads();
-    const int npix = dw * dh;
-    for (int i = tid; i < npix; i += 256) {
-        int yy = i / dw, xx = i - yy * dw;
-        const uint8_t* p = tile + (yy + 3) * tp + (xx + 3);
-        int circ[16];
-        circ[0] = p[3 * tp];
-        circ[1] = p[3 * tp + 1];
-        circ[2] = p[2 * tp + 2];
-        circ[3] = p[tp + 3];
-        circ[4] = p[3];
-        circ[5] = p[-tp + 3];
-        circ[6] = p[-2 * tp + 2];
-        circ[7] = p[-3 * tp + 1];
-        circ[8] = p[-3 * tp];
-        circ[9] = p[-3 * tp - 1];
-        circ[10] = p[-2 * tp - 2];
-        circ[11] = p[-tp - 3];
-        circ[12] = p[-3];
-        circ[13] = p[tp - 3];
-        circ[14] = p[2 * tp - 2];
-        circ[15] = p[3 * tp - 1];
-        Sb[i] = (uint8_t)fast_strength(p[0], circ, g.tmin);
-    }
-    __syncthreads();
-    // raster-order chunk per thread for the ordered compaction
-    const int chunk = (npix + 255) / 256;
-    const int p0 = min(tid * chunk, npix), p1 = min(p0 + chunk, npix);
+    const int sh = (int)((uintptr_t)roi & 3);
+    const uint32_t* src = (const uint32_t*)(roi - sh);
+    const int tw = (sh + cg.hx + 3) >> 2;  // words per tile row
+    const int TP = tw * 4;                 // tile row pitch in bytes
+    const int dwp = (dw + 3) & ~3;         // S / flag row pitch
+    const int nw = (dh * dwp) >> 2;        // words of the S (and flag) plane
+    uint32_t* tile = (uint32_t*)smem;
+    uint8_t* tb = smem + sh;                             // tb[y * TP + x] = ROI pixel (x, y)
+    uint8_t* Sb = smem + cg.hy * TP;                     // dh x dwp strengths (0 = not a corner)
+    uint8_t* Fl = Sb + dh * dwp;                         // dh x dwp keep flags
+    uint32_t* L = (uint32_t*)(Fl + dh * dwp);            // queued corners (y << 16 | x)
+    uint32_t* Q = L + FAST_LCAP;                         // queued pre-filter survivors
+    int* rowc = (int*)(Q + FAST_QCAP);                   // dh row counts / offsets
+    stage_rows_to_lds(tile, tw, src, lg.pitch >> 2, cg.hy, tw, tw, wave, lane);
     int t = g.fastTh;
-    int mine = 0;
-    for (int i = p0; i < p1; ++i) {
-        int yy = i / dw, xx = i - yy * dw;
-        mine += nms_keep(Sb, dw, dh, xx, yy, t);
-    }
-    s_cnt[tid] = mine;
-    __syncthreads();
-    if (tid == 0) {
-        int s = 0;
-        for (int i = 0; i < 256; ++i) s += s_cnt[i];
-        s_total = s;
-    }
-    __syncthreads();
-    if (s_total <= 3) {
-        t = 7;
-        mine = 0;
-        for (int i = p0; i < p1; ++i) {
-            int yy = i / dw, xx = i - yy * dw;
-            mine += nms_keep(Sb, dw, dh, xx, yy, t);
+    for (int pass = 0; pass < 2; ++pass) {
+        for (int i = tid; i < nw; i += 256) {
+            ((uint32_t*)Sb)[i] = 0u;
+            ((uint32_t*)Fl)[i] = 0u;
         }
-        __syncthreads();
-        s_cnt[tid] = mine;
-        __syncthreads();
         if (tid == 0) {
-            int s = 0;
-            for (int i = 0; i < 256; ++i) s += s_cnt[i];
-            s_total = s;
+            s_nL = 0;
+            s_nQ = 0;
+            s_total = 0;
         }
         __syncthreads();
-    }
-    // exclusive scan of per-thread counts (256 entries, one wave does it)
-    if (tid < 64) {
-        int v0 = s_cnt[4 * tid], v1 = s_cnt[4 * tid + 1], v2 = s_cnt[4 * tid + 2], v3 = s_cnt[4 * tid + 3];
-        int sum = v0 + v1 + v2 + v3, incl = sum;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            int n = __shfl_up(incl, o, 64);
-            if (tid >= o) incl += n;
+        // detect, stage 1: compass pre-filter over every pixel; survivors are queued in Q
+        // (overflow beyond FAST_QCAP is tested in place, in wave segments)
+        for (int yy = wave; yy < dh; yy += 4) {
+            const uint8_t* rowp = tb + (yy + 3) * TP + 3;
+            for (int xb = 0; xb < dw; xb += 64) {
+                const int xx = xb + lane;
+                const bool act = xx < dw;
+                const uint8_t* p = rowp + (act ? xx : 0);
+                const int v = p[0];
+                const int hi = v + t, lo = v - t;
+                const int q0 = p[3 * TP], q4 = p[3], q8 = p[-3 * TP], q12 = p[-3];
+                const int bm = (q0 > hi) | ((q4 > hi) << 1) | ((q8 > hi) << 2) | ((q12 > hi) << 3);
+                const int dm = (q0 < lo) | ((q4 < lo) << 1) | ((q8 < lo) << 2) | ((q12 < lo) << 3);
+                const bool pre = act && (((bm & ((bm >> 1) | (bm << 3))) | (dm & ((dm >> 1) | (dm << 3)))) & 0xF);
+                if (pre) {
+                    const int pos = atomicAdd(&s_nQ, 1);
+                    if (pos < FAST_QCAP) {
+                        Q[pos] = ((uint32_t)yy << 16) | (uint32_t)xx;
+                    } else if (fast_is_corner(p, TP, t)) {
+                        const int lp = atomicAdd(&s_nL, 1);
+                        if (lp < FAST_LCAP)
+                            L[lp] = ((uint32_t)yy << 16) | (uint32_t)xx;
+                        else
+                            Sb[yy * dwp + xx] = (uint8_t)fast_exact_strength(p, TP);
+                    }
+                }
+            }
         }
-        int ex = incl - sum;
-        s_cnt[4 * tid] = ex;
-        s_cnt[4 * tid + 1] = ex + v0;
-        s_cnt[4 * tid + 2] = ex + v0 + v1;
-        s_cnt[4 * tid + 3] = ex + v0 + v1 + v2;
+        __syncthreads();
+        // detect, stage 2: full 16-point 9-arc test on the queued pixels, all lanes busy
+        {
+            const int nq = min(s_nQ, FAST_QCAP);
+            for (int i = tid; i < nq; i += 256) {
+                const int yy = (int)(Q[i] >> 16), xx = (int)(Q[i] & 0xFFFF);
+                const uint8_t* p = tb + (yy + 3) * TP + 3 + xx;
+                if (fast_is_corner(p, TP, t)) {
+                    const int lp = atomicAdd(&s_nL, 1);
+                    if (lp < FAST_LCAP)
+                        L[lp] = Q[i];
+                    else
+                        Sb[yy * dwp + xx] = (uint8_t)fast_exact_strength(p, TP);
+                }
+            }
+        }
+        __syncthreads();
+        const int nQ = s_nL, nL = min(nQ, FAST_LCAP);
+        for (int i = tid; i < nL; i += 256) {
+            const int yy = (int)(L[i] >> 16), xx = (int)(L[i] & 0xFFFF);
+            Sb[yy * dwp + xx] = (uint8_t)fast_exact_strength(tb + (yy + 3) * TP + 3 + xx, TP);
+        }
+        __syncthreads();
+        // non-max suppression around every corner (all pixels when the queue overflowed)
+        int kept = 0;
+        const int nN = nQ > FAST_LCAP ? dh * dw : nL;
+        for (int i = tid; i < nN; i += 256) {
+            int yy, xx;
+            if (nQ > FAST_LCAP) {
+                yy = i / dw;
+                xx = i - yy * dw;
+            } else {
+                yy = (int)(L[i] >> 16);
+                xx = (int)(L[i] & 0xFFFF);
+            }
+            const int s0 = Sb[yy * dwp + xx];
+            if (s0 <= t) continue;
+            bool keep = true;
+#pragma unroll
+            for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+                for (int dx = -1; dx <= 1; ++dx) {
+                    if (dx == 0 && dy == 0) continue;
+                    const int nx = xx + dx, ny = yy + dy;
+                    const int n = (nx >= 0 && nx < dw && ny >= 0 && ny < dh) ? Sb[ny * dwp + nx] : 0;
+                    keep = keep && (s0 - 1 > (n > t ? n - 1 : 0));
+                }
+            if (keep) {
+                Fl[yy * dwp + xx] = 1;
+                ++kept;
+            }
+        }
+        if (kept) atomicAdd(&s_total, kept);
+        __syncthreads();
+        if (pass == 0 && s_total <= 3) {
+            t = 7;
+            __syncthreads();
+            continue;
+        }
+        break;
+    }
+    // raster-order compaction from the flag plane: row counts, scan, write
+    const uint32_t* Flw = (const uint32_t*)Fl;
+    const int rw = dwp >> 2;
+    for (int yy = wave; yy < dh; yy += 4) {
+        int cnt = 0;
+        for (int w = lane; w < rw; w += 64) cnt += __popc(Flw[yy * rw + w]);
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+        if (lane == 0) rowc[yy] = cnt;
+    }
+    __syncthreads();
+    if (wave == 0) {
+        int carry = 0;
+        for (int r0 = 0; r0 < dh; r0 += 64) {
+            const int r = r0 + lane;
+            const int v = r < dh ? rowc[r] : 0;
+            int incl = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int nb = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += nb;
+            }
+            if (r < dh) rowc[r] = carry + incl - v;
+            carry += __shfl(incl, 63, 64);
+        }
+        if (lane == 0) *outCount = carry;
     }
     __syncthreads();
     uint32_t* out = cand + (long long)b * g.candPerFrame + cg.candOff;
-    int pos = s_cnt[tid];
-    for (int i = p0; i < p1; ++i) {
-        int yy = i / dw, xx = i - yy * dw;
-        if (nms_keep(Sb, dw, dh, xx, yy, t)) {
-            int sc = Sb[i] - 1;
-            int lx = cg.x0 + 3 + xx, ly = cg.y0 + 3 + yy;
-            out[pos++] = ((uint32_t)sc << 24) | ((uint32_t)ly << 12) | (uint32_t)lx;
+    for (int yy = wave; yy < dh; yy += 4) {
+        int off = rowc[yy];
+        const uint32_t ly = (uint32_t)(cg.y0 + 3 + yy) << 12;
+        for (int w0 = 0; w0 < rw; w0 += 64) {
+            const int w = w0 + lane;
+            const uint32_t f = w < rw ? Flw[yy * rw + w] : 0u;
+            const int n = __popc(f);
+            int incl = n;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int nb = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += nb;
+            }
+            int pos = off + incl - n;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if ((f >> (8 * j)) & 1u) {
+                    const int xx = 4 * w + j;
+                    const uint32_t sc = (uint32_t)(Sb[yy * dwp + xx] - 1);
+                    out[pos++] = (sc << 24) | ly | (uint32_t)(cg.x0 + 3 + xx);
+                }
+            off += __shfl(incl, 63, 64);
         }
     }
-    if (tid == 0) *outCount = s_total;
 }
 
 // ---- selection (retainBest replay) -------------------------------------------------------
@@ -411,62 +592,143 @@ __global__ void __launch_bounds__(64) k_select(uint32_t* __restrict__ cand, cons
     if (lane == 0) lvlCount[(long long)b * g.L + l] = keep;
 }
 
-// ---- orientation + descriptor -------------------------------------------------------------
-// One wave per keypoint.  A 43x43 patch around the keypoint (the 31x31 IC disc, the rBRIEF
-// samples' |offset| <= 18 and the 7x7 blur taps) is staged in LDS from the padded level.
-#define DESC_R 21
-#define DESC_P 43
-#define DESC_PITCH 44
+// ---- descriptor image: GaussianBlur(level ROI, 7x7, sigma 2) in place ---------------------
+// The reference blurs the level ROI in place right before its descriptors
+// (ORBextractor.cc:760): samples inside the ROI read the blur, samples in the 16-px padding
+// read the un-blurred reflect-101 border (rBRIEF reaches 2 px into it).  k_blur materialises
+// exactly that image over level coordinates [-3, w+3) x [-3, h+3) in a buffer laid out like
+// the pyramid.  Fixed-point taps (18,34,49,55,49,34,18)/256 per axis:
+// T = sum_j k_j sum_i k_i P; columns x < 4*floor(w/4) round T/65536 half-to-even (the SSE2
+// SymmColumnVec_32s8u float path), the tail columns half-up ((T + 2^15) >> 16).
+#define BLUR_TW 256  // output columns per tile: 64 lanes x 4 pixels
+#define BLUR_RW 16   // output rows per wave
+#define BLUR_TH 64   // output rows per tile (4 waves)
+#define BLUR_IW 66   // LDS row pitch in dwords: tile columns x0-4 .. x0+259
+struct BlurTile {
+    int level, x0, y0;  // tile origin in level coordinates: x0 = -4 + 256 k, y0 = -3 + 64 m
+};
 
-__global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__ pyr, Geom g,
+__device__ __forceinline__ int byte_of(uint32_t w, int k) { return (int)((w >> (8 * k)) & 0xFFu); }
+
+__global__ void __launch_bounds__(256) k_blur(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur, Geom g,
+                                              const BlurTile* __restrict__ tiles) {
+    __shared__ __attribute__((aligned(16))) uint32_t s_in[(BLUR_TH + 6) * BLUR_IW];
+    const BlurTile t = tiles[blockIdx.x];
+    const int b = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const LevelGeom& lg = g.lv[t.level];
+    const uint8_t* src = pyr + lg.base + (long long)b * lg.fstride;
+    uint8_t* dst = blur + lg.base + (long long)b * lg.fstride;
+    // input rows y0-3 .. y0+TH+2, columns x0-4 .. x0+259 (padded +16: dword aligned).  Rows
+    // past the padded buffer are only needed by rows that are never written: not loaded.
+    const int py0 = t.y0 - 3 + EDGE, px0 = t.x0 - 4 + EDGE;
+    const int rows = min(BLUR_TH + 6, lg.ph - py0);
+    const int spw = lg.pitch >> 2;
+    stage_rows_to_lds(s_in, BLUR_IW, (const uint32_t*)(src + (long long)py0 * lg.pitch + px0), spw, rows, BLUR_IW,
+                      spw - (px0 >> 2), wave, lane);
+    __syncthreads();
+    const int x = t.x0 + 4 * lane;  // first of this lane's 4 output columns
+    if (x >= lg.w + 4) return;
+    const int k0 = g.taps[0], k1 = g.taps[1], k2 = g.taps[2], k3 = g.taps[3];
+    const uint32_t* in = s_in + (wave * BLUR_RW) * BLUR_IW + lane;
+    int R[7][4];
+    uint32_t C[7];  // raw centre dword of each ring row
+#pragma unroll
+    for (int r = 0; r < BLUR_RW + 6; ++r) {
+        const uint32_t d0 = in[r * BLUR_IW], d1 = in[r * BLUR_IW + 1], d2 = in[r * BLUR_IW + 2];
+        int B[12];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            B[k] = byte_of(d0, k);
+            B[4 + k] = byte_of(d1, k);
+            B[8 + k] = byte_of(d2, k);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            R[r % 7][j] = k0 * B[4 + j] + k1 * (B[3 + j] + B[5 + j]) + k2 * (B[2 + j] + B[6 + j]) +
+                          k3 * (B[1 + j] + B[7 + j]);
+        C[r % 7] = d1;
+        if (r < 6) continue;
+        const int y = t.y0 + wave * BLUR_RW + (r - 6);  // output row; ring row (r - 3) is its centre
+        if (y >= lg.h + 3) break;
+        const bool rowIn = y >= 0 && y < lg.h;
+        const uint32_t craw = C[(r - 3) % 7];
+        uint32_t word = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int xj = x + j;
+            int v;
+            if (rowIn && xj >= 0 && xj < lg.w) {
+                const int T = k0 * R[(r - 3) % 7][j] + k1 * (R[(r - 4) % 7][j] + R[(r - 2) % 7][j]) +
+                              k2 * (R[(r - 5) % 7][j] + R[(r - 1) % 7][j]) + k3 * (R[(r - 6) % 7][j] + R[r % 7][j]);
+                v = xj < lg.xsimd_blur ? (T + 32767 + ((T >> 16) & 1)) >> 16 : (T + 32768) >> 16;
+                v = min(v, 255);
+            } else {
+                v = byte_of(craw, j);  // outside the ROI: the un-blurred padding
+            }
+            word |= (uint32_t)v << (8 * j);
+        }
+        *(uint32_t*)(dst + (long long)(y + EDGE) * lg.pitch + (x + EDGE)) = word;
+    }
+}
+
+// ---- orientation + descriptor -------------------------------------------------------------
+// One wave per keypoint.  IC angle on the raw level (31x31 disc staged in LDS with dword
+// loads); the 512 rBRIEF samples read the descriptor image built by k_blur.
+#define IC_P 36  // LDS pitch of the 31-row IC patch
+
+__global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__ pyr,
+                                                     const uint8_t* __restrict__ blur, Geom g,
                                                      const uint32_t* __restrict__ lvlOut,
                                                      const int* __restrict__ lvlCount, orb_keypoint_t* __restrict__ kps,
                                                      uint8_t* __restrict__ desc, int* __restrict__ counts) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_patch[4][DESC_P * DESC_PITCH];
+    __shared__ __attribute__((aligned(16))) uint32_t s_patch[4][31 * IC_P / 4];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int b = blockIdx.y;
     const int k = blockIdx.x * 4 + wave;
     // locate the level of keypoint k (level-major output order, ORBextractor.cc:749-778)
-    int l = -1, off = 0, total = 0, idx = 0;
+    int l = -1, total = 0, idx = 0;
     for (int i = 0; i < g.L; ++i) {
-        int cnt = lvlCount[(long long)b * g.L + i];
+        const int cnt = lvlCount[(long long)b * g.L + i];
         if (l < 0 && k < total + cnt) {
             l = i;
             idx = k - total;
-            off = total;
         }
         total += cnt;
     }
     if (k == 0 && lane == 0) counts[b] = total;
-    (void)off;
     const bool valid = l >= 0;  // wave-uniform; every wave still reaches the barrier below
     const LevelGeom& lg = g.lv[valid ? l : 0];
     const uint32_t e = valid ? lvlOut[(long long)b * g.kpCap + lg.kpBase + idx] : 0u;
     const int x = e & 0xFFF, y = (e >> 12) & 0xFFF, score = e >> 24;
-    const uint8_t* lvl = pyr + lg.base + (long long)b * lg.fstride;
-    uint8_t* P = s_patch[wave];
-    // patch rows y-21 .. y+21, cols x-21 .. x+21 (padded coordinates +16)
+    const long long fbase = lg.base + (long long)b * lg.fstride;
+    // raw 31x31 patch, rows y-15..y+15, cols x-15..x+15 (dword-aligned spans)
+    const uint8_t* p0 = pyr + fbase + (long long)(y + EDGE - HALF_PATCH) * lg.pitch + (x + EDGE - HALF_PATCH);
+    const int sh = (int)((uintptr_t)p0 & 3);
+    const uint32_t* w0 = (const uint32_t*)(p0 - sh);
+    const int spw = lg.pitch >> 2;
+    uint32_t* P = s_patch[wave];
     if (valid)
-        for (int i = lane; i < DESC_P * DESC_P; i += 64) {
-            int r = i / DESC_P, cc = i - r * DESC_P;
-            P[r * DESC_PITCH + cc] = lvl[(long long)(y + EDGE - DESC_R + r) * lg.pitch + (x + EDGE - DESC_R + cc)];
+        for (int i = lane; i < 31 * 9; i += 64) {
+            const int r = i / 9, c = i - r * 9;
+            P[r * (IC_P / 4) + c] = w0[(long long)r * spw + c];
         }
     __syncthreads();
     if (!valid) return;
+    const uint8_t* Pb = (const uint8_t*)P + sh + HALF_PATCH;  // Pb[r * IC_P + u], u in [-15, 15]
     // IC_Angle (ORBextractor.cc:124-151): lanes 0..30 take rows v = lane - 15
     int m01 = 0, m10 = 0;
     if (lane < 31) {
-        int v = lane - HALF_PATCH;
-        int d = g.umax[v < 0 ? -v : v];
-        const uint8_t* row = P + (DESC_R + v) * DESC_PITCH + DESC_R;
-        int su = 0, s = 0;
+        const int v = lane - HALF_PATCH;
+        const int d = g.umax[v < 0 ? -v : v];
+        const uint8_t* row = Pb + lane * IC_P;
+        int su = 0, sm = 0;
         for (int u = -d; u <= d; ++u) {
-            int val = row[u];
+            const int val = row[u];
             su += u * val;
-            s += val;
+            sm += val;
         }
         m10 = su;
-        m01 = v * s;
+        m01 = v * sm;
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
@@ -479,33 +741,21 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
     float sa, ca;
     glibc_sincosf(angle * factorPI, &sa, &ca);
     const float a = ca, bsin = sa;
-    const int k0 = g.taps[0], k1 = g.taps[1], k2 = g.taps[2], k3 = g.taps[3];
-    auto sample = [&](int idx_pt) -> int {
-        float px = (float)c_pattern[2 * idx_pt], py = (float)c_pattern[2 * idx_pt + 1];
-        int dy = (int)rintf(__builtin_fmaf(px, bsin, py * a));
-        int dx = (int)rintf(__builtin_fmaf(px, a, -(py * bsin)));
-        int sx = x + dx, sy = y + dy;
-        const uint8_t* q = P + (DESC_R + dy) * DESC_PITCH + (DESC_R + dx);
-        if (sx < 0 || sx >= lg.w || sy < 0 || sy >= lg.h) return q[0];  // un-blurred padding
-        int T = 0;
+    const uint8_t* center = blur + fbase + (long long)(y + EDGE) * lg.pitch + (x + EDGE);
+    const int pitch = lg.pitch;
+    int vals[8];
 #pragma unroll
-        for (int j = -3; j <= 3; ++j) {
-            const uint8_t* r = q + j * DESC_PITCH;
-            int R = k0 * r[0] + k1 * (r[-1] + r[1]) + k2 * (r[-2] + r[2]) + k3 * (r[-3] + r[3]);
-            int kj = j == 0 ? k0 : (j == 1 || j == -1) ? k1 : (j == 2 || j == -2) ? k2 : k3;
-            T += kj * R;
-        }
-        int v = sx < lg.xsimd_blur ? (T + 32767 + ((T >> 16) & 1)) >> 16 : (T + 32768) >> 16;
-        return min(v, 255);
-    };
+    for (int q = 0; q < 8; ++q) {
+        const int pt = lane * 8 + q;  // pattern point: tests 4*lane .. 4*lane+3
+        const float px = (float)c_pattern[2 * pt], py = (float)c_pattern[2 * pt + 1];
+        const int dy = (int)rintf(__builtin_fmaf(px, bsin, py * a));
+        const int dx = (int)rintf(__builtin_fmaf(px, a, -(py * bsin)));
+        vals[q] = center[(long long)dy * pitch + dx];
+    }
     int nib = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        int test = lane * 4 + q;  // bit (test & 7) of byte test >> 3
-        int t0 = sample(2 * test), t1 = sample(2 * test + 1);
-        nib |= (t0 < t1) << q;
-    }
-    int other = __shfl_xor(nib, 1, 64);
+    for (int q = 0; q < 4; ++q) nib |= (vals[2 * q] < vals[2 * q + 1]) << q;
+    const int other = __shfl_xor(nib, 1, 64);
     const long long kslot = (long long)b * g.kpCap + k;
     if ((lane & 1) == 0) desc[kslot * 32 + (lane >> 1)] = (uint8_t)(nib | (other << 4));
     if (lane == 0) {
@@ -527,160 +777,274 @@ struct MatchGeom {
     float invW, invH;  // FRAME_GRID_COLS / (maxX - minX), FRAME_GRID_ROWS / (maxY - minY)
 };
 
-// One wave per frame pair.  F2's octave-0, in-grid keypoints (the only possible candidates of
-// GetFeaturesInArea(x, y, window, 0, 0), Frame.cc:200-265) are staged in LDS with their grid
-// cell; F1's octave-0 keypoints are then processed in index order, sequentially, as the
-// reference's greedy loop requires (vMatchedDistance / vnMatches21 feed later queries).  For
-// each query the candidate set is evaluated in parallel and reduced to (best, first-in-grid-
-// traversal-order argmin, second-best) — the values the reference's sequential scan produces.
-__global__ void __launch_bounds__(64) k_match_init(const orb_keypoint_t* __restrict__ kps,
-                                                   const uint8_t* __restrict__ desc, const int* __restrict__ counts,
-                                                   int cap, int n2max, const int* __restrict__ pf1,
-                                                   const int* __restrict__ pf2, MatchGeom mg, float nnratio,
-                                                   int checkOri, float r, float* __restrict__ prev,
-                                                   int* __restrict__ m12out, int* __restrict__ nmOut) {
+// One workgroup (4 waves) per frame pair.
+//   phase 0  F2's octave-0, in-grid keypoints — the only possible candidates of
+//            GetFeaturesInArea(x, y, window, 0, 0) (Frame.cc:200-265) — are staged in LDS,
+//            ranked by grid-traversal order (ix, iy, index: Frame.cc:233-258), so a slot
+//            number IS the reference's candidate order; F1's octave-0 queries are listed in
+//            index order.
+//   phase 1  (parallel) every query's window candidates are scored; each keeps its 8
+//            smallest keys (dist << 11 | slot) = the reference's (distance, first-in-order).
+//   phase 2  (one wave, sequential: vMatchedDistance / vnMatches21 feed later queries)
+//            best = first candidate with vMatchedDistance > dist, second = the next such;
+//            if a truncated top-8 holds < 2 such candidates the wave rescans the window.
+//   phase 3  rotation histogram, ComputeThreeMaxima, vnMatches12 / vbPrevMatched out.
+#define MATCH_TOPK 8
+__device__ __forceinline__ void topk_insert(uint32_t (&t)[MATCH_TOPK], uint32_t key) {
+#pragma unroll
+    for (int i = 0; i < MATCH_TOPK; ++i) {
+        uint32_t lo = min(t[i], key), hi = max(t[i], key);
+        t[i] = lo;
+        key = hi;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_match_init(const orb_keypoint_t* __restrict__ kps,
+                                                    const uint8_t* __restrict__ desc, const int* __restrict__ counts,
+                                                    int cap, int nmax, const int* __restrict__ pf1,
+                                                    const int* __restrict__ pf2, MatchGeom mg, float nnratio,
+                                                    int checkOri, float r, float* __restrict__ prev,
+                                                    int* __restrict__ m12out, int* __restrict__ nmOut) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int p = blockIdx.x, lane = threadIdx.x;
+    __shared__ int s_n2c, s_n1c;
+    __shared__ int s_hist[32];
+    __shared__ int s_ind[3];
+    const int p = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int f1 = pf1[p], f2 = pf2[p];
     const int n1 = counts[f1], n2 = counts[f2];
     const orb_keypoint_t* K1 = kps + (long long)f1 * cap;
     const orb_keypoint_t* K2 = kps + (long long)f2 * cap;
     const uint32_t* D1 = (const uint32_t*)(desc + (long long)f1 * cap * 32);
     const uint32_t* D2 = (const uint32_t*)(desc + (long long)f2 * cap * 32);
-    uint32_t* s_d2 = (uint32_t*)smem;                    // n2max x 8
-    float* s_x2 = (float*)(s_d2 + (size_t)n2max * 8);    // n2max
-    float* s_y2 = s_x2 + n2max;                          // n2max
-    int* s_cell = (int*)(s_y2 + n2max);                  // posX * 48 + posY
-    int* s_idx = s_cell + n2max;                         // original index i2
-    int* s_md = s_idx + n2max;                           // vMatchedDistance
-    int* s_m21 = s_md + n2max;                           // vnMatches21
-    int* s_m12 = s_m21 + n2max;                          // vnMatches12 (cap)
-    signed char* s_bin = (signed char*)(s_m12 + cap);    // rotation bin of accepted i1 (cap)
-    __shared__ int s_n2c;
-    __shared__ int s_hist[32];
-    __shared__ int s_ind[3];
-    // stage F2 candidates (octave 0, PosInGrid true), preserving index order
-    int base = 0;
-    for (int i0 = 0; i0 < n2; i0 += 64) {
-        int i2 = i0 + lane;
-        bool ok = false;
-        int px = 0, py = 0;
-        if (i2 < n2) {
-            orb_keypoint_t kp = K2[i2];
-            px = (int)roundf((kp.x - mg.minX) * mg.invW);
-            py = (int)roundf((kp.y - mg.minY) * mg.invH);
-            ok = kp.octave == 0 && !(px < 0 || px >= 64 || py < 0 || py >= 48);
-        }
-        unsigned long long m = __ballot(ok);
-        int slot = base + __popcll(m & ((1ull << lane) - 1ull));
-        if (ok && slot < n2max) {
-            orb_keypoint_t kp = K2[i2];
-            s_x2[slot] = kp.x;
-            s_y2[slot] = kp.y;
-            s_cell[slot] = px * 48 + py;
-            s_idx[slot] = i2;
-            s_md[slot] = 0x7fffffff;
-            s_m21[slot] = -1;
-#pragma unroll
-            for (int w = 0; w < 8; ++w) s_d2[slot * 8 + w] = D2[(long long)i2 * 8 + w];
-        }
-        base += __popcll(m);
+    uint32_t* s_d2 = (uint32_t*)smem;              // nmax x 8
+    float* s_x2 = (float*)(s_d2 + (size_t)nmax * 8);
+    float* s_y2 = s_x2 + nmax;
+    int* s_cell = (int*)(s_y2 + nmax);              // posX * 48 + posY
+    int* s_idx = s_cell + nmax;                     // i2
+    int* s_md = s_idx + nmax;                       // vMatchedDistance
+    int* s_m21 = s_md + nmax;                       // vnMatches21
+    int* s_q2i = s_m21 + nmax;                      // query -> i1
+    float* s_qx = (float*)(s_q2i + nmax);
+    float* s_qy = s_qx + nmax;
+    float* s_qa = s_qy + nmax;                      // query angle
+    float* s_a2 = s_qa + nmax;                      // F2 slot angle
+    uint32_t* s_list = (uint32_t*)(s_a2 + nmax);    // nmax x TOPK
+    int* s_lcnt = (int*)(s_list + (size_t)nmax * MATCH_TOPK);
+    int* s_m12 = s_lcnt + nmax;                     // vnMatches12 (cap)
+    signed char* s_bin = (signed char*)(s_m12 + cap);  // rotation bin of accepted i1 (cap)
+    uint32_t* s_key = s_list;                       // phase-0 scratch (cap <= 8 * nmax)
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    // ---- phase 0: keys in parallel, then ordered compaction from LDS ----
+    // s_key[i2] = traversal key of F2 keypoint i2 or ~0 (not octave 0 / outside the grid);
+    // s_m12[i1] = 1 if F1 keypoint i1 is a query (octave 0), as scratch.
+    for (int i = tid; i < n2; i += 256) {
+        const orb_keypoint_t kp = K2[i];
+        const int px = (int)roundf((kp.x - mg.minX) * mg.invW);
+        const int py = (int)roundf((kp.y - mg.minY) * mg.invH);
+        const bool ok = kp.octave == 0 && !(px < 0 || px >= 64 || py < 0 || py >= 48);
+        s_key[i] = ok ? (((uint32_t)(px * 48 + py) << 16) | (uint32_t)i) : 0xFFFFFFFFu;
     }
-    if (lane == 0) s_n2c = min(base, n2max);
-    for (int i = lane; i < n1; i += 64) {
+    for (int i = tid; i < n1; i += 256) s_m12[i] = K1[i].octave == 0;  // level1 > 0 -> continue (ORBmatcher.cc:615)
+    __syncthreads();
+    if (wave == 0) {  // in-place, in-order compaction (one wave: reads precede writes)
+        int base = 0;
+        for (int i0 = 0; i0 < n2; i0 += 64) {
+            const uint32_t key = i0 + lane < n2 ? s_key[i0 + lane] : 0xFFFFFFFFu;
+            const bool ok = key != 0xFFFFFFFFu;
+            const uint64_t m = __ballot(ok);
+            if (ok) s_key[base + __popcll(m & below)] = key;
+            base += __popcll(m);
+        }
+        if (lane == 0) s_n2c = base;
+    } else if (wave == 1) {
+        int base = 0;
+        for (int i0 = 0; i0 < n1; i0 += 64) {
+            const int i1 = i0 + lane;
+            const bool ok = i1 < n1 && s_m12[i1];
+            const uint64_t m = __ballot(ok);
+            if (ok && base + __popcll(m & below) < nmax) s_q2i[base + __popcll(m & below)] = i1;
+            base += __popcll(m);
+        }
+        if (lane == 0) s_n1c = base;
+    }
+    __syncthreads();
+    const int n2c = s_n2c, n1c = s_n1c;
+    if (n2c > nmax || n1c > nmax) {  // capacity exceeded: report, never truncate silently
+        if (tid == 0) nmOut[p] = -1;
+        return;
+    }
+    // rank F2 candidates by traversal key -> slot
+    for (int t = tid; t < n2c; t += 256) {
+        const uint32_t k = s_key[t];
+        int rank = 0;
+        for (int u = 0; u < n2c; ++u) rank += s_key[u] < k;
+        const int i2 = (int)(k & 0xFFFF);
+        const orb_keypoint_t kp = K2[i2];
+        s_x2[rank] = kp.x;
+        s_y2[rank] = kp.y;
+        s_a2[rank] = kp.angle;
+        s_cell[rank] = (int)(k >> 16);
+        s_idx[rank] = i2;
+        s_md[rank] = 0x7fffffff;
+        s_m21[rank] = -1;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) s_d2[rank * 8 + w] = D2[(long long)i2 * 8 + w];
+    }
+    for (int q = tid; q < n1c; q += 256) {
+        const int i1 = s_q2i[q];
+        const orb_keypoint_t kp = K1[i1];
+        s_qx[q] = prev ? prev[((long long)p * cap + i1) * 2] : kp.x;
+        s_qy[q] = prev ? prev[((long long)p * cap + i1) * 2 + 1] : kp.y;
+        s_qa[q] = kp.angle;
+    }
+    __syncthreads();
+    for (int i = tid; i < n1; i += 256) {
         s_m12[i] = -1;
         s_bin[i] = -1;
     }
     __syncthreads();
-    const int n2c = s_n2c;
-    for (int i1 = 0; i1 < n1; ++i1) {
-        const orb_keypoint_t kp1 = K1[i1];
-        if (kp1.octave != 0) continue;  // level1 > 0 (octave < 0 rejected by the host API)
-        const float qx = prev ? prev[((long long)p * cap + i1) * 2] : kp1.x;
-        const float qy = prev ? prev[((long long)p * cap + i1) * 2 + 1] : kp1.y;
-        int minCX = max(0, (int)floorf((qx - mg.minX - r) * mg.invW));
-        int maxCX = min(63, (int)ceilf((qx - mg.minX + r) * mg.invW));
-        int minCY = max(0, (int)floorf((qy - mg.minY - r) * mg.invH));
-        int maxCY = min(47, (int)ceilf((qy - mg.minY + r) * mg.invH));
-        if (minCX > maxCX || minCY > maxCY) continue;
-        uint32_t d1[8];
+    // ---- phase 1: per-query top-8 (dist, order) ----
+    for (int q0 = 0; q0 < n1c; q0 += 256) {
+        const int q = q0 + tid;
+        const bool act = q < n1c;
+        float qx = 0.f, qy = 0.f;
+        int minCX = 1, maxCX = 0, minCY = 1, maxCY = 0;
+        uint32_t d1[8] = {};
+        if (act) {
+            qx = s_qx[q];
+            qy = s_qy[q];
+            minCX = max(0, (int)floorf((qx - mg.minX - r) * mg.invW));
+            maxCX = min(63, (int)ceilf((qx - mg.minX + r) * mg.invW));
+            minCY = max(0, (int)floorf((qy - mg.minY - r) * mg.invH));
+            maxCY = min(47, (int)ceilf((qy - mg.minY + r) * mg.invH));
+            const int i1 = s_q2i[q];
 #pragma unroll
-        for (int w = 0; w < 8; ++w) d1[w] = D1[(long long)i1 * 8 + w];
-        // lane-local best (dist, traversal order, slot) and second-best distance
-        unsigned long long lbest = ~0ull;
-        int lsecond = 0x7fffffff;
-        for (int j = lane; j < n2c; j += 64) {
-            int cell = s_cell[j];
-            int cx = cell / 48, cy = cell - cx * 48;
+            for (int w = 0; w < 8; ++w) d1[w] = D1[(long long)i1 * 8 + w];
+        }
+        uint32_t top[MATCH_TOPK];
+#pragma unroll
+        for (int k = 0; k < MATCH_TOPK; ++k) top[k] = 0xFFFFFFFFu;
+        int cnt = 0;
+        for (int j = 0; j < n2c; ++j) {  // uniform j: LDS broadcast reads
+            const int cell = s_cell[j];
+            const int cx = cell / 48, cy = cell - cx * 48;
             if (cx < minCX || cx > maxCX || cy < minCY || cy > maxCY) continue;
             if (fabsf(s_x2[j] - qx) > r || fabsf(s_y2[j] - qy) > r) continue;
-            int dist = hamming256(d1, s_d2 + j * 8);
-            if (s_md[j] <= dist) continue;
-            unsigned long long key = ((unsigned long long)dist << 40) |
-                                     ((unsigned long long)((cell << 16) | s_idx[j]) << 11) | (unsigned long long)j;
-            if (key < lbest) {
-                if (lbest != ~0ull) lsecond = (int)(lbest >> 40);
-                lbest = key;
-            } else if (dist < lsecond) {
-                lsecond = dist;
-            }
+            const int dist = hamming256(d1, s_d2 + j * 8);
+            topk_insert(top, ((uint32_t)dist << 11) | (uint32_t)j);
+            ++cnt;
         }
-        unsigned long long gbest = lbest;
+        if (act) {
 #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            unsigned long long v = __shfl_xor(gbest, o, 64);
-            gbest = v < gbest ? v : gbest;
-        }
-        if (gbest == ~0ull) continue;  // no candidate
-        int contrib = (lbest == gbest) ? lsecond : (lbest == ~0ull ? 0x7fffffff : (int)(lbest >> 40));
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) contrib = min(contrib, __shfl_xor(contrib, o, 64));
-        const int bestDist = (int)(gbest >> 40);
-        const int bestSlot = (int)(gbest & 0x7FF);
-        if (bestDist <= 50 && (float)bestDist < (float)contrib * nnratio) {
-            if (lane == 0) {
-                const int bestIdx2 = s_idx[bestSlot];
-                int old = s_m21[bestSlot];
-                if (old >= 0) s_m12[old] = -1;
-                s_m12[i1] = bestIdx2;
-                s_m21[bestSlot] = i1;
-                s_md[bestSlot] = bestDist;
-                if (checkOri) {
-                    float rot = kp1.angle - K2[bestIdx2].angle;
-                    if (rot < 0.0f) rot += 360.0f;
-                    int bin = (int)roundf(rot * (1.0f / 30));
-                    if (bin == 30) bin = 0;
-                    s_bin[i1] = (signed char)bin;
-                }
-            }
-            __syncthreads();
+            for (int k = 0; k < MATCH_TOPK; ++k) s_list[q * MATCH_TOPK + k] = top[k];
+            s_lcnt[q] = cnt;
         }
     }
     __syncthreads();
+    // ---- phase 2: the sequential greedy pass (ORBmatcher.cc:611-680) ----
+    if (wave == 0) {
+        for (int q = 0; q < n1c; ++q) {
+            const int cnt = s_lcnt[q];
+            if (cnt == 0) continue;  // vIndices2.empty()
+            const int i1 = s_q2i[q];
+            const int k = min(cnt, MATCH_TOPK);
+            const uint32_t e = lane < k ? s_list[q * MATCH_TOPK + lane] : 0xFFFFFFFFu;
+            const bool valid = lane < k && s_md[e & 0x7FF] > (int)(e >> 11);
+            uint64_t m = __ballot(valid);
+            uint32_t best;
+            int second;
+            if (__popcll(m) >= 2 || cnt <= MATCH_TOPK) {
+                if (m == 0) continue;  // every candidate already held at <= its distance
+                const int e1 = __ffsll((unsigned long long)m) - 1;
+                best = __shfl(e, e1, 64);
+                const uint64_t m2 = m & (m - 1);
+                second = m2 ? (int)(__shfl(e, __ffsll((unsigned long long)m2) - 1, 64) >> 11) : 0x7fffffff;
+            } else {
+                // exact rescan of the whole window
+                const float qx = s_qx[q], qy = s_qy[q];
+                const int minCX = max(0, (int)floorf((qx - mg.minX - r) * mg.invW));
+                const int maxCX = min(63, (int)ceilf((qx - mg.minX + r) * mg.invW));
+                const int minCY = max(0, (int)floorf((qy - mg.minY - r) * mg.invH));
+                const int maxCY = min(47, (int)ceilf((qy - mg.minY + r) * mg.invH));
+                uint32_t d1[8];
+#pragma unroll
+                for (int w = 0; w < 8; ++w) d1[w] = D1[(long long)i1 * 8 + w];
+                uint32_t lb = 0xFFFFFFFFu;
+                int ls = 0x7fffffff;
+                for (int j = lane; j < n2c; j += 64) {
+                    const int cell = s_cell[j];
+                    const int cx = cell / 48, cy = cell - cx * 48;
+                    if (cx < minCX || cx > maxCX || cy < minCY || cy > maxCY) continue;
+                    if (fabsf(s_x2[j] - qx) > r || fabsf(s_y2[j] - qy) > r) continue;
+                    const int dist = hamming256(d1, s_d2 + j * 8);
+                    if (s_md[j] <= dist) continue;
+                    const uint32_t key = ((uint32_t)dist << 11) | (uint32_t)j;
+                    if (key < lb) {
+                        if (lb != 0xFFFFFFFFu) ls = (int)(lb >> 11);
+                        lb = key;
+                    } else if (dist < ls) {
+                        ls = dist;
+                    }
+                }
+                uint32_t gb = lb;
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) gb = min(gb, (uint32_t)__shfl_xor((int)gb, o, 64));
+                if (gb == 0xFFFFFFFFu) continue;
+                int contrib = (lb == gb) ? ls : (lb == 0xFFFFFFFFu ? 0x7fffffff : (int)(lb >> 11));
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) contrib = min(contrib, __shfl_xor(contrib, o, 64));
+                best = gb;
+                second = contrib;
+            }
+            const int bestDist = (int)(best >> 11);
+            const int bestSlot = (int)(best & 0x7FF);
+            if (bestDist <= 50 && (float)bestDist < (float)second * nnratio) {
+                if (lane == 0) {
+                    const int bestIdx2 = s_idx[bestSlot];
+                    const int old = s_m21[bestSlot];
+                    if (old >= 0) s_m12[old] = -1;
+                    s_m12[i1] = bestIdx2;
+                    s_m21[bestSlot] = i1;
+                    s_md[bestSlot] = bestDist;
+                    if (checkOri) {
+                        float rot = s_qa[q] - s_a2[bestSlot];
+                        if (rot < 0.0f) rot += 360.0f;
+                        int bin = (int)roundf(rot * (1.0f / 30));
+                        if (bin == 30) bin = 0;
+                        s_bin[i1] = (signed char)bin;
+                    }
+                }
+                // lane 0's LDS writes land before any lane's next read (same wave, in order)
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            }
+        }
+    }
+    __syncthreads();
+    // ---- phase 3 ----
     if (checkOri) {
-        if (lane < 32) s_hist[lane] = 0;
+        if (tid < 32) s_hist[tid] = 0;
         __syncthreads();
-        for (int i = lane; i < n1; i += 64)
+        for (int i = tid; i < n1; i += 256)
             if (s_bin[i] >= 0) atomicAdd(&s_hist[(int)s_bin[i]], 1);
         __syncthreads();
-        if (lane == 0) {  // ComputeThreeMaxima (ORBmatcher.cc:1748-1789)
+        if (tid == 0) {  // ComputeThreeMaxima (ORBmatcher.cc:1748-1789)
             int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
             for (int i = 0; i < 30; ++i) {
-                const int s = s_hist[i];
-                if (s > max1) {
+                const int sz = s_hist[i];
+                if (sz > max1) {
                     max3 = max2;
                     max2 = max1;
-                    max1 = s;
+                    max1 = sz;
                     ind3 = ind2;
                     ind2 = ind1;
                     ind1 = i;
-                } else if (s > max2) {
+                } else if (sz > max2) {
                     max3 = max2;
-                    max2 = s;
+                    max2 = sz;
                     ind3 = ind2;
                     ind2 = i;
-                } else if (s > max3) {
-                    max3 = s;
+                } else if (sz > max3) {
+                    max3 = sz;
                     ind3 = i;
                 }
             }
@@ -696,15 +1060,15 @@ __global__ void __launch_bounds__(64) k_match_init(const orb_keypoint_t* __restr
         }
         __syncthreads();
         const int i1x = s_ind[0], i2x = s_ind[1], i3x = s_ind[2];
-        for (int i = lane; i < n1; i += 64) {
-            int bn = s_bin[i];
+        for (int i = tid; i < n1; i += 256) {
+            const int bn = s_bin[i];
             if (bn >= 0 && bn != i1x && bn != i2x && bn != i3x) s_m12[i] = -1;
         }
         __syncthreads();
     }
     int nm = 0;
-    for (int i = lane; i < n1; i += 64) {
-        int m = s_m12[i];
+    for (int i = tid; i < n1; i += 256) {
+        const int m = s_m12[i];
         m12out[(long long)p * cap + i] = m;
         if (m >= 0) {
             nm++;
@@ -716,7 +1080,9 @@ __global__ void __launch_bounds__(64) k_match_init(const orb_keypoint_t* __restr
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) nm += __shfl_xor(nm, o, 64);
-    if (lane == 0) nmOut[p] = nm;
+    if (lane == 0) s_hist[wave] = nm;
+    __syncthreads();
+    if (tid == 0) nmOut[p] = s_hist[0] + s_hist[1] + s_hist[2] + s_hist[3];
 }
 
 // ======================================================================================
@@ -760,6 +1126,9 @@ struct orb_extractor {
     size_t cellLds = 0;
     // device workspace
     uint8_t* d_pyr = nullptr;
+    uint8_t* d_blur = nullptr;
+    BlurTile* d_tiles = nullptr;
+    int nTiles = 0;
     uint32_t* d_cand = nullptr;
     int* d_cellCount = nullptr;
     uint32_t* d_lvl = nullptr;
@@ -767,7 +1136,7 @@ struct orb_extractor {
     int* d_rtab = nullptr;
     CellGeom* d_cells = nullptr;
     // per-stage HIP-event timing (orb_profile_*): stage k brackets its kernel(s) on the launch stream
-    static constexpr int kStages = 5;
+    static constexpr int kStages = 6;
     bool prof = false;
     std::vector<hipEvent_t> evPool;  // 2 per stage per launch, recycled after each read
     std::vector<std::pair<int, int>> evPending;  // (stage, index of the start event)
@@ -789,6 +1158,8 @@ struct orb_extractor {
 
     void free_ws() {
         hipFree(d_pyr);
+        hipFree(d_blur);
+        hipFree(d_tiles);
         hipFree(d_cand);
         hipFree(d_cellCount);
         hipFree(d_lvl);
@@ -800,6 +1171,9 @@ struct orb_extractor {
         hipFree(d_desc);
         hipFree(d_counts);
         d_pyr = nullptr;
+        d_blur = nullptr;
+        d_tiles = nullptr;
+        nTiles = 0;
         d_cand = nullptr;
         d_cellCount = nullptr;
         d_lvl = nullptr;
@@ -933,7 +1307,10 @@ struct orb_extractor {
                                 return set_err(ORB_ENOTSUP, "cell ROI outside the level (the reference asserts)");
                             int dw = c.hx - 6, dh = c.hy - 6;
                             c.cap = (dw > 0 && dh > 0) ? ((dw + 1) / 2) * ((dh + 1) / 2) : 0;
-                            size_t lds = (size_t)((c.hx + 3) & ~3) * c.hy + (size_t)std::max(dw, 0) * std::max(dh, 0);
+                            const size_t dwp = (size_t)((std::max(dw, 0) + 3) & ~3);
+                            size_t lds = (size_t)(((c.hx + 3 + 3) >> 2) * 4) * c.hy +
+                                         2 * dwp * std::max(dh, 0) + 4 * (FAST_LCAP + FAST_QCAP) +
+                                         4 * (size_t)std::max(dh, 0) + 16;
                             cellLds = std::max(cellLds, lds);
                         }
                     }
@@ -994,6 +1371,14 @@ struct orb_extractor {
         G.kpCap = kpCap;
         // workspace
         HIP_TRY(hipMalloc(&d_pyr, (size_t)pyrBytes));
+        HIP_TRY(hipMalloc(&d_blur, (size_t)pyrBytes));
+        std::vector<BlurTile> tl;
+        for (int l = 0; l < nlevels; ++l)
+            for (int y0 = -3; y0 < G.lv[l].h + 3; y0 += BLUR_TH)
+                for (int x0 = -4; x0 < G.lv[l].w + 4; x0 += BLUR_TW) tl.push_back(BlurTile{l, x0, y0});
+        HIP_TRY(hipMalloc(&d_tiles, tl.size() * sizeof(BlurTile)));
+        HIP_TRY(hipMemcpy(d_tiles, tl.data(), tl.size() * sizeof(BlurTile), hipMemcpyHostToDevice));
+        nTiles = (int)tl.size();
         HIP_TRY(hipMalloc(&d_cand, (size_t)std::max(cand, 1) * maxBatch * 4));
         HIP_TRY(hipMalloc(&d_cellCount, (size_t)G.nCells * maxBatch * 4));
         HIP_TRY(hipMalloc(&d_lvl, (size_t)std::max(kpCap, 1) * maxBatch * 4));
@@ -1061,15 +1446,15 @@ struct orb_extractor {
         stage_begin(0, st);
         {
             const LevelGeom& lg = g.lv[0];
-            dim3 grid((lg.pitch / 4 + 255) / 256, lg.ph, B);
-            hipLaunchKernelGGL(k_pyr0, grid, dim3(256), 0, st, d_imgs, stride, fpitch, d_pyr, g);
+            dim3 grid((lg.pitch / 4 + 63) / 64, (lg.ph + 3) / 4, B);
+            hipLaunchKernelGGL(k_pyr0, grid, dim3(64, 4), 0, st, d_imgs, stride, fpitch, d_pyr, g);
         }
         stage_end(st);
         stage_begin(1, st);
         for (int l = 1; l < nlevels; ++l) {
             const LevelGeom& lg = g.lv[l];
-            dim3 grid((lg.pitch / 4 + 255) / 256, lg.ph, B);
-            hipLaunchKernelGGL(k_pyr_resize, grid, dim3(256), 0, st, d_pyr, d_rtab, g, l);
+            dim3 grid((lg.pitch / 4 + 63) / 64, (lg.ph + 4 * PYR_RW - 1) / (4 * PYR_RW), B);
+            hipLaunchKernelGGL(k_pyr_resize, grid, dim3(64, 4), 0, st, d_pyr, d_rtab, g, l);
         }
         stage_end(st);
         stage_begin(2, st);
@@ -1081,8 +1466,12 @@ struct orb_extractor {
                            d_lvlCount);
         stage_end(st);
         stage_begin(4, st);
+        hipLaunchKernelGGL(k_blur, dim3(nTiles, B), dim3(256), 0, st, d_pyr, d_blur, g, d_tiles);
+        stage_end(st);
+        stage_begin(5, st);
         dim3 gd((std::max(kpCap, 1) + 3) / 4, B);
-        hipLaunchKernelGGL(k_orient_desc, gd, dim3(256), 0, st, d_pyr, g, d_lvl, d_lvlCount, kps, desc, counts);
+        hipLaunchKernelGGL(k_orient_desc, gd, dim3(256), 0, st, d_pyr, d_blur, g, d_lvl, d_lvlCount, kps, desc,
+                           counts);
         stage_end(st);
         HIP_TRY(hipGetLastError());
         return ORB_OK;
@@ -1243,8 +1632,10 @@ int orb_descriptor_distance(const uint8_t* a, const uint8_t* b) {
     return dist;
 }
 
-static size_t match_lds_bytes(int cap, int n2max) {
-    return (size_t)n2max * (32 + 4 * 6) + (size_t)cap * 4 + (size_t)cap + 16;
+static size_t match_lds_bytes(int cap, int nmax) {
+    // F2 slots (desc 32 + x,y,a,cell,idx,md,m21 28) + queries (q2i,qx,qy,qa 16 + top-8 32 + cnt 4)
+    // + cap x (m12 4 + bin 1)
+    return (size_t)nmax * (56 + 56) + (size_t)cap * 5 + 16;
 }
 
 int orb_search_for_initialization_batch_device(const orb_keypoint_t* d_kps, const uint8_t* d_desc,
@@ -1257,13 +1648,14 @@ int orb_search_for_initialization_batch_device(const orb_keypoint_t* d_kps, cons
         return set_err(ORB_EINVAL, "bad arguments");
     if (P == 0) return ORB_OK;
     if (bounds.max_x <= bounds.min_x || bounds.max_y <= bounds.min_y) return set_err(ORB_EINVAL, "bad bounds");
-    const int n2max = std::min(cap, 2047);
-    size_t lds = match_lds_bytes(cap, n2max);
-    if (lds > 160 * 1024 - 256) return set_err(ORB_ENOTSUP, "per-frame keypoint capacity too large for LDS");
+    const int nmax = std::min(cap, 1024);  // octave-0 keypoints per frame held in LDS
+    if (cap > 8 * nmax) return set_err(ORB_ENOTSUP, "per-frame keypoint capacity too large");
+    size_t lds = match_lds_bytes(cap, nmax);
+    if (lds > 160 * 1024 - 512) return set_err(ORB_ENOTSUP, "per-frame keypoint capacity too large for LDS");
     MatchGeom mg{bounds.min_x, bounds.max_x, bounds.min_y, bounds.max_y,
                  static_cast<float>(64) / static_cast<float>(bounds.max_x - bounds.min_x),
                  static_cast<float>(48) / static_cast<float>(bounds.max_y - bounds.min_y)};
-    hipLaunchKernelGGL(k_match_init, dim3(P), dim3(64), lds, (hipStream_t)stream, d_kps, d_desc, d_counts, cap, n2max,
+    hipLaunchKernelGGL(k_match_init, dim3(P), dim3(256), lds, (hipStream_t)stream, d_kps, d_desc, d_counts, cap, nmax,
                        d_pair_f1, d_pair_f2, mg, nnratio, check_ori, (float)window, d_prev_xy, d_matches12,
                        d_nmatches);
     HIP_TRY(hipGetLastError());
@@ -1281,7 +1673,7 @@ int orb_search_for_initialization(const orb_keypoint_t* kps1, const uint8_t* des
     *n_matches = 0;
     if (n1 == 0) return ORB_OK;
     const int cap = std::max(std::max(n1, n2), 1);
-    if (n2 > 2047) return set_err(ORB_ENOTSUP, "F2 has more than 2047 keypoints");
+    if (n1 > 8192 || n2 > 8192) return set_err(ORB_ENOTSUP, "more than 8192 keypoints in a frame");
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));
     orb_keypoint_t* dk = nullptr;
@@ -1327,11 +1719,12 @@ int orb_search_for_initialization(const orb_keypoint_t* kps1, const uint8_t* des
         e = hipMemcpy(prev_xy, dp, (size_t)n1 * 8, hipMemcpyDeviceToHost);
     cleanup();
     if (e != hipSuccess) return set_err(ORB_EDEVICE, std::string("match: ") + hipGetErrorString(e));
+    if (nm < 0) return set_err(ORB_ENOTSUP, "more than 1024 octave-0 keypoints in a frame");
     *n_matches = nm;
     return ORB_OK;
 }
 
-static const char* kStageNames[] = {"k_pyr0", "k_pyr_resize", "k_fast_cells", "k_select", "k_orient_desc"};
+static const char* kStageNames[] = {"k_pyr0", "k_pyr_resize", "k_fast_cells", "k_select", "k_blur", "k_orient_desc"};
 
 int orb_profile_enable(orb_extractor_t* h, int enable) {
     if (!h) return set_err(ORB_EINVAL, "bad handle");
@@ -1381,6 +1774,17 @@ int orb_debug_level_image(orb_extractor_t* h, int b, int l, uint8_t* out, int* w
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy2D(out, lg.w + 32, h->d_pyr + lg.base + (long long)b * lg.fstride, lg.pitch, lg.w + 32, lg.ph,
+                        hipMemcpyDeviceToHost));
+    return ORB_OK;
+}
+
+// Descriptor image of level l, frame b (blurred ROI + raw padding ring), padded layout.
+int orb_debug_blur_image(orb_extractor_t* h, int b, int l, uint8_t* out) {
+    if (!h || l < 0 || l >= h->nlevels || !h->d_blur) return set_err(ORB_EINVAL, "bad arguments");
+    const LevelGeom& lg = h->g.lv[l];
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy2D(out, lg.w + 32, h->d_blur + lg.base + (long long)b * lg.fstride, lg.pitch, lg.w + 32, lg.ph,
                         hipMemcpyDeviceToHost));
     return ORB_OK;
 }

@@ -52,6 +52,10 @@ def lib() -> ctypes.CDLL:
                                                 ctypes.POINTER(i)]
         L.oracle_search_by_bow_kf_kf.argtypes = [vp, vp, i, vp, vp, vp, vp, i, vp, vp, i, vp, vp, vp, vp, i, f, i,
                                                  vp, ctypes.POINTER(i)]
+        L.oracle_rot_bin.argtypes = [f, f]
+        L.oracle_resize.argtypes = [vp, i, i, i, vp, i, i, i]
+        L.oracle_blur_padded.argtypes = [vp, i, i, vp]
+        L.oracle_fast.argtypes = [vp, i, i, i, i, vp, i]
         L.oracle_bench.restype = ctypes.c_double
         L.oracle_bench.argtypes = [i, f, i, i, vp, i, i, i, i, ctypes.c_int64, i, i, ctypes.POINTER(ctypes.c_int64),
                                    ctypes.POINTER(ctypes.c_int64)]

@@ -1,0 +1,81 @@
+"""The drop-in boundary without a GPU: libraries load, every declared C symbol is exported,
+argument validation fails loudly, and host-only entry points work."""
+import ctypes
+import pathlib
+import re
+
+import numpy as np
+import pytest
+
+import orbslam_jpminipc_amd as orb
+from orbslam_jpminipc_amd import _native
+
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+
+
+def declared_functions(header: pathlib.Path):
+    text = re.sub(r"/\*.*?\*/", "", header.read_text(), flags=re.S)
+    return sorted(set(re.findall(r"^[A-Za-z_][\w \*]*?\b(orb_\w+|oracle_\w+)\s*\(", text, flags=re.M)))
+
+
+def exported(so: pathlib.Path):
+    lib = ctypes.CDLL(str(so))
+    return lib
+
+
+def test_hip_library_exports_every_abi_symbol():
+    names = declared_functions(ROOT / "include" / "orb_abi.h")
+    assert "orb_extract" in names and "orb_search_for_initialization_batch_device" in names
+    lib = orb.hip_lib()
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    # the Python binding table covers the whole header
+    assert set(names) <= set(_native.HIP_SIGNATURES)
+
+
+def test_oracle_library_exports_every_symbol():
+    names = declared_functions(ROOT / "oracle" / "orb_oracle.h")
+    lib = exported(ROOT / "oracle" / "liborb_oracle.so")
+    assert [n for n in names if not hasattr(lib, n)] == []
+
+
+def test_version_string():
+    assert orb.hip_lib().orb_version().decode().startswith("orb_hip gfx950")
+
+
+def test_bad_parameters_fail_loudly():
+    with pytest.raises(orb.OrbError) as e:
+        orb.ORBextractor(0, 1.2, 8)
+    assert e.value.code == _native.ORB_EINVAL
+    with pytest.raises(orb.OrbError):
+        orb.ORBextractor(1000, 1.0, 8)  # scaleFactor must be > 1
+    with pytest.raises(orb.OrbError):
+        orb.ORBextractor(1000, 1.2, 99)
+
+
+def test_product_does_not_reference_the_oracle():
+    # the product library and package never load or link the checker
+    so = (ROOT / "orbslam_jpminipc_amd" / "liborb_hip.so").read_bytes()
+    assert b"liborb_oracle" not in so and b"oracle_extract" not in so
+    for py in (ROOT / "orbslam_jpminipc_amd").glob("*.py"):
+        assert "oracle" not in py.read_text().replace("oracle/", ""), py
+
+
+def test_keypoint_record_layout():
+    assert _native.KEYPOINT_DTYPE.itemsize == 28
+    assert [f for f in _native.KEYPOINT_DTYPE.names] == ["x", "y", "size", "angle", "response", "octave", "class_id"]
+
+
+def test_synth_is_deterministic_and_consecutive_frames_overlap():
+    a = orb.synth_stream(320, 240, stream=3, first=0, count=3)
+    b = orb.synth_stream(320, 240, stream=3, first=1, count=2)
+    assert np.array_equal(a[1:], b)
+    c = orb.synth_stream(320, 240, stream=4, first=0, count=1)
+    assert not np.array_equal(a[0], c[0])
+    # frame t+1 is frame t shifted by (dx, dy) in [-6, 6]^2 up to the +-8 noise
+    f0, f1 = a[0].astype(int), a[1].astype(int)
+    best = min(
+        (np.abs(f0[16:-16, 16:-16] - f1[16 + dy:224 + dy, 16 + dx:304 + dx]).mean(), dx, dy)
+        for dx in range(-6, 7) for dy in range(-6, 7))
+    assert best[0] < 6.0
+    assert orb.synth_special(orb.SYN_FLAT, 64, 48).max() == 128

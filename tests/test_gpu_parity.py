@@ -103,6 +103,36 @@ def test_extract_parity_fast_thresholds():
         _check_frame(ext, ora, orb.synth_stream(640, 480, stream=21, count=1)[0])
 
 
+@pytest.mark.parametrize("W,H", [(640, 480), (1241, 376), (161, 121)])
+def test_pyramid_and_descriptor_image_parity(W, H):
+    """Every pyramid level (padded) and every descriptor image (blurred ROI + the raw ring
+    rBRIEF can reach) against the oracle's ComputePyramid / GaussianBlur restatement."""
+    nl = 8 if W >= 320 else 4
+    ext = orb.ORBextractor(1000 if W >= 320 else 300, 1.2, nl, orb.FAST_SCORE, 20, device=0)
+    ora = Oracle(1000 if W >= 320 else 300, 1.2, nl, 1, 20)
+    img = orb.synth_stream(W, H, stream=13, count=1)[0]
+    ext(img)
+    ora.extract(img)
+    lib = orb.hip_lib()
+    for l in range(nl):
+        w, h = ctypes.c_int(), ctypes.c_int()
+        lib.orb_debug_level_image(ext._h, 0, l, None, ctypes.byref(w), ctypes.byref(h))
+        w, h = w.value, h.value
+        g = np.empty((h + 32, w + 32), np.uint8)
+        lib.orb_debug_level_image(ext._h, 0, l, g.ctypes.data_as(ctypes.c_void_p), None, None)
+        o = ora.level_image(l)
+        assert np.array_equal(g, o), f"level {l} pyramid differs at {np.argwhere(g != o)[:5]}"
+        bl = np.empty((h + 32, w + 32), np.uint8)
+        lib.orb_debug_blur_image(ext._h, 0, l, bl.ctypes.data_as(ctypes.c_void_p))
+        ob = np.empty((h, w), np.uint8)
+        if ora.L.oracle_level_blurred(ora.h, l, ob.ctypes.data_as(ctypes.c_void_p)) == 0:
+            assert np.array_equal(bl[16:16 + h, 16:16 + w], ob), f"level {l} blur differs"
+        ring = np.zeros_like(bl, bool)
+        ring[14:h + 18, 14:w + 18] = True
+        ring[16:16 + h, 16:16 + w] = False
+        assert np.array_equal(bl[ring], o[ring]), f"level {l} descriptor-image padding differs"
+
+
 def test_empty_image_returns_untouched():
     ext = orb.ORBextractor(1000, 1.2, 8, orb.FAST_SCORE, 20, device=0)
     assert ext(np.zeros((0, 0), np.uint8)) == (None, None)
