@@ -79,3 +79,15 @@ def test_synth_is_deterministic_and_consecutive_frames_overlap():
         for dx in range(-6, 7) for dy in range(-6, 7))
     assert best[0] < 6.0
     assert orb.synth_special(orb.SYN_FLAT, 64, 48).max() == 128
+
+
+def test_cpp_facade_compiles_and_fails_loudly():
+    """include/orb_slam_gpu.hpp (the reference-class facade) builds against liborb_hip.so."""
+    import subprocess
+
+    pkg = ROOT / "orbslam_jpminipc_amd"
+    exe = pathlib.Path("/tmp/orb_facade_check")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-o", str(exe), str(ROOT / "tests/native/facade_check.cpp"),
+                    f"-L{pkg}", "-lorb_hip", f"-Wl,-rpath,{pkg}", "-Wl,-rpath-link,/opt/rocm/lib"], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
