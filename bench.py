@@ -53,13 +53,14 @@ def stage_bytes(W, H, n_kp, n_cand, n_pairs_kp0, B):
     lv = level_sizes(W, H)
     pad = [(w + 32) * (h + 32) for w, h in lv]
     px = [w * h for w, h in lv]
-    det = [max(w - 26, 0) * max(h - 26, 0) for w, h in lv]  # cell ROIs: detection area + 3 px halo
     return {
         "k_pyr0": B * (W * H + pad[0]),
         "k_pyr_resize": B * sum(px[l - 1] + pad[l] for l in range(1, len(lv))) / (len(lv) - 1),  # per launch
-        "k_fast_cells": B * sum(det) + 4 * n_cand,
+        # blur + FAST: read the level with its 3/4 px halo once, write the blurred ROI + border
+        "k_level": B * sum(2 * (w + 8) * (h + 6) for w, h in lv),
+        # read the level corner lists (>= survivors), write the cell candidates
+        "k_cell_nms": 8 * n_cand,
         "k_select": 8 * n_cand + 4 * n_kp,
-        "k_blur": B * sum((w + 12) * (h + 12) + (w + 6) * (h + 6) for w, h in lv),
         "k_orient_desc": n_kp * (4 + 31 * 31 + 512 + 60),
     }
 

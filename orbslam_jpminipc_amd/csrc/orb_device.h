@@ -14,7 +14,7 @@ constexpr int EDGE = 16;           // EDGE_THRESHOLD, ORBextractor.cc:77
 constexpr int HALF_PATCH = 15;     // HALF_PATCH_SIZE, ORBextractor.cc:76
 
 // cv::borderInterpolate(p, len, BORDER_REFLECT_101) (OpenCV 2.4).
-__device__ __forceinline__ int reflect101(int p, int len) {
+__host__ __device__ __forceinline__ int reflect101(int p, int len) {
     if ((unsigned)p < (unsigned)len) return p;
     if (len == 1) return 0;
     do {

@@ -3,10 +3,12 @@
 // Pipeline for a batch of B same-size frames (all device-resident, one HIP stream):
 //   k_pyr0        level 0 + reflect-101 padding          (ORBextractor.cc:814-815)
 //   k_pyr_resize  level l from level l-1, fused padding   (ORBextractor.cc:800-807), l = 1..L-1
-//   k_fast_cells  per-cell FAST(th) / FAST(7) + 3x3 NMS + raster-order compaction
-//                                                          (ORBextractor.cc:560-614)
-//   k_select      per (frame, level): quota redistribution, retainBest per cell, level
-//                 retainBest — exact libstdc++ nth_element replay (ORBextractor.cc:622-701)
+//   k_level       per level tile: descriptor image (7x7 blur of the ROI, ORBextractor.cc:760)
+//                 and FAST at fastTh with the per-cell 3x3 NMS; survivors appended to their
+//                 cell's slots                              (ORBextractor.cc:560-607)
+//   k_select      per (frame, level): FAST(7) re-run of cells with <= 3 survivors (609-614),
+//                 raster order per cell, quota redistribution, retainBest per cell and per
+//                 level — exact libstdc++ nth_element replay (ORBextractor.cc:622-701)
 //   k_orient_desc per keypoint (one wave): IC angle on the raw level, rBRIEF on the
 //                 7x7 sigma-2 blur evaluated at the sample points, keypoint record
 //                                                          (ORBextractor.cc:124-194, 705-777)
@@ -64,8 +66,11 @@ struct LevelGeom {
     int xsimd_blur;         // 4 * floor(w / 4): GaussianBlur SSE2 columns
     int xs_resize, xmax;    // VResizeLinear SSE2 columns, HResizeLinear xmax (l >= 1)
     int rtab;               // offset of this level's resize table (int32 units), l >= 1
+    int rtile;              // offset of this level's resize tile table (4 ints per tile), l >= 1
     float scale;            // mvScaleFactor[l]
     float size;             // (int)(31 * mvScaleFactor[l])
+    int cellW, cellH;       // detection-area size of the (non-last) cells: corner -> cell bucket
+    int detX1, detY1;       // FAST detection region [16, detX1) x [16, detY1): union of the cells' areas
 };
 
 struct Geom {
@@ -73,7 +78,7 @@ struct Geom {
     int nCells;        // cells per frame (all levels)
     int candPerFrame;  // candidate slots per frame (u32)
     int kpCap;         // keypoint slots per frame (sum of nDesired)
-    int fastTh, tmin;  // clamped fastTh, min(fastTh, 7)
+    int fastTh;        // clamped to [0, 255]
     int scoreType;
     int taps[4];       // Gaussian 7-tap fixed-point kernel, centre first: 55, 49, 34, 18
     int umax[16];
@@ -86,6 +91,7 @@ struct CellGeom {
     int cap;             // max NMS survivors: ceil(dw/2) * ceil(dh/2)
     int candOff;         // offset in the frame's candidate area
     int skipped;         // reference `continue` on hX/hY <= 0 (nTotal stays 0, bNoMore false)
+    int cornerOff;       // bucket of this cell's FAST corners in the frame's corner area (dw*dh slots)
 };
 
 // ======================================================================================
@@ -113,74 +119,6 @@ __global__ void __launch_bounds__(256) k_pyr0(const uint8_t* __restrict__ imgs, 
         word |= v << (8 * i);
     }
     *(uint32_t*)(pyr + lg.base + (long long)b * lg.fstride + (long long)py * lg.pitch + x4) = word;
-}
-
-// Level l >= 1: cv::resize(level l-1, (w_l, h_l), INTER_LINEAR) for 8U (SURVEY.md A2):
-// fixed-point HResizeLinear rows; vertical SSE2 body (VResizeLinearVec_32s8u) for x < xs,
-// scalar FixedPtCast<int,uchar,22> tail; then copyMakeBorder(REFLECT_101 | ISOLATED), fused
-// by evaluating the resize at the reflected coordinate of every padded pixel.  A thread owns
-// 4 padded columns (coefficients kept in registers) and walks PYR_RW padded rows.
-#define PYR_RW 16
-__global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, const int* __restrict__ rtab, Geom g,
-                                                    int l) {
-    const LevelGeom& lg = g.lv[l];
-    const LevelGeom& ls = g.lv[l - 1];
-    const int b = blockIdx.z;
-    const int x4 = (blockIdx.x * 64 + threadIdx.x) * 4;
-    const int py0 = (blockIdx.y * 4 + threadIdx.y) * PYR_RW;
-    if (x4 >= lg.pitch || py0 >= lg.ph) return;
-    const int* xofs = rtab + lg.rtab;
-    const int* alpha = xofs + lg.w;
-    const int* yofs = alpha + lg.w;
-    const int* beta = yofs + lg.h;
-    int sx[4], a0[4], a1[4];
-    bool live[4], simd[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int px = x4 + i;
-        live[i] = px < lg.w + 2 * EDGE;
-        const int lx = reflect101(min(px, lg.w + 2 * EDGE - 1) - EDGE, lg.w);
-        sx[i] = xofs[lx];
-        if (lx < lg.xmax) {
-            const int aa = alpha[lx];
-            a0[i] = (short)(aa & 0xFFFF);
-            a1[i] = (short)(aa >> 16);
-        } else {  // HResizeLinear tail: S[sx] * ONE
-            a0[i] = 2048;
-            a1[i] = 0;
-        }
-        simd[i] = lx < lg.xs_resize;
-    }
-    const uint8_t* S = pyr + ls.base + (long long)b * ls.fstride + (long long)EDGE * ls.pitch + EDGE;
-    uint8_t* D = pyr + lg.base + (long long)b * lg.fstride + x4;
-    const int py1 = min(py0 + PYR_RW, lg.ph);
-    for (int py = py0; py < py1; ++py) {
-        const int ly = reflect101(py - EDGE, lg.h);
-        const int sy = yofs[ly];
-        const int bb = beta[ly];
-        const int b0 = (short)(bb & 0xFFFF), b1 = (short)(bb >> 16);
-        const uint8_t* S0 = S + (long long)min(max(sy, 0), ls.h - 1) * ls.pitch;
-        const uint8_t* S1 = S + (long long)min(max(sy + 1, 0), ls.h - 1) * ls.pitch;
-        uint32_t word = 0;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            // a1 == 0 on the tail columns, where sx + 1 may be past the row: index sx instead
-            const int sx1 = a1[i] ? sx[i] + 1 : sx[i];
-            const int H0 = S0[sx[i]] * a0[i] + S0[sx1] * a1[i];
-            const int H1 = S1[sx[i]] * a0[i] + S1[sx1] * a1[i];
-            int r;
-            if (simd[i]) {
-                const int h0 = min(max(H0 >> 4, -32768), 32767), h1 = min(max(H1 >> 4, -32768), 32767);
-                int sm = min(max(((h0 * b0) >> 16) + ((h1 * b1) >> 16), -32768), 32767);
-                sm = min(max(sm + 2, -32768), 32767);
-                r = sm >> 2;
-            } else {
-                r = (H0 * b0 + H1 * b1 + (1 << 21)) >> 22;
-            }
-            word |= (live[i] ? (uint32_t)min(max(r, 0), 255) : 0u) << (8 * i);
-        }
-        *(uint32_t*)(D + (long long)py * lg.pitch) = word;
-    }
 }
 
 // ---- global -> LDS staging --------------------------------------------------------------
@@ -211,6 +149,86 @@ __device__ __forceinline__ void stage_rows_to_lds(uint32_t* __restrict__ dst, in
     }
 }
 
+// Level l >= 1: cv::resize(level l-1, (w_l, h_l), INTER_LINEAR) for 8U (SURVEY.md A2):
+// fixed-point HResizeLinear rows; vertical SSE2 body (VResizeLinearVec_32s8u) for x < xs,
+// scalar FixedPtCast<int,uchar,22> tail; then copyMakeBorder(REFLECT_101 | ISOLATED), fused
+// by evaluating the resize at the reflected coordinate of every padded pixel.
+// One workgroup per RZ_TW x RZ_TH tile of the padded level: the source rectangle the tile
+// reads (host table: first dword column, dwords, first row, rows) is staged into LDS with
+// coalesced dword loads; a thread owns 4 padded columns (taps in registers) and walks the
+// RZ_TH / 4 rows of its wave, gathering the 2x2 taps from LDS.
+#define RZ_TW 256
+#define RZ_TH 32
+__global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, const int* __restrict__ rtab, Geom g,
+                                                    int l) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_src[];
+    const LevelGeom& lg = g.lv[l];
+    const LevelGeom& ls = g.lv[l - 1];
+    const int b = blockIdx.z, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int* tt = rtab + lg.rtile + 4 * (blockIdx.y * gridDim.x + blockIdx.x);
+    const int colStart = tt[0], words = tt[1], rowMin = tt[2], nrows = tt[3];
+    const uint8_t* S = pyr + ls.base + (long long)b * ls.fstride + (long long)EDGE * ls.pitch + EDGE;
+    stage_rows_to_lds(s_src, words, (const uint32_t*)(S + (long long)rowMin * ls.pitch + colStart), ls.pitch >> 2,
+                      nrows, words, words, wave, lane);
+    const int* xofs = rtab + lg.rtab;
+    const int* alpha = xofs + lg.w;
+    const int* yofs = alpha + lg.w;
+    const int* beta = yofs + lg.h;
+    const int x4 = blockIdx.x * RZ_TW + 4 * lane;
+    int o0[4], o1[4], a0[4], a1[4];
+    bool live[4], simd[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int px = x4 + i;
+        live[i] = px < lg.w + 2 * EDGE;
+        const int lx = reflect101(min(px, lg.w + 2 * EDGE - 1) - EDGE, lg.w);
+        const int sx = xofs[lx];
+        if (lx < lg.xmax) {
+            const int aa = alpha[lx];
+            a0[i] = (short)(aa & 0xFFFF);
+            a1[i] = (short)(aa >> 16);
+        } else {  // HResizeLinear tail: S[sx] * ONE (sx + 1 may be past the row: not read)
+            a0[i] = 2048;
+            a1[i] = 0;
+        }
+        o0[i] = sx - colStart;
+        o1[i] = (a1[i] ? sx + 1 : sx) - colStart;
+        simd[i] = lx < lg.xs_resize;
+    }
+    __syncthreads();
+    if (x4 >= lg.pitch) return;
+    const uint8_t* L = (const uint8_t*)s_src;
+    const int LP = words * 4;
+    uint8_t* D = pyr + lg.base + (long long)b * lg.fstride + x4;
+    const int pyA = blockIdx.y * RZ_TH + wave * (RZ_TH / 4);
+    const int pyB = min(pyA + RZ_TH / 4, lg.ph);
+    for (int py = pyA; py < pyB; ++py) {
+        const int ly = reflect101(py - EDGE, lg.h);
+        const int sy = yofs[ly];
+        const int bb = beta[ly];
+        const int b0 = (short)(bb & 0xFFFF), b1 = (short)(bb >> 16);
+        const uint8_t* L0 = L + (min(max(sy, 0), ls.h - 1) - rowMin) * LP;
+        const uint8_t* L1 = L + (min(max(sy + 1, 0), ls.h - 1) - rowMin) * LP;
+        uint32_t word = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int H0 = L0[o0[i]] * a0[i] + L0[o1[i]] * a1[i];
+            const int H1 = L1[o0[i]] * a0[i] + L1[o1[i]] * a1[i];
+            int r;
+            if (simd[i]) {
+                const int h0 = min(max(H0 >> 4, -32768), 32767), h1 = min(max(H1 >> 4, -32768), 32767);
+                int sm = min(max(((h0 * b0) >> 16) + ((h1 * b1) >> 16), -32768), 32767);
+                sm = min(max(sm + 2, -32768), 32767);
+                r = sm >> 2;
+            } else {
+                r = (H0 * b0 + H1 * b1 + (1 << 21)) >> 22;
+            }
+            word |= (live[i] ? (uint32_t)min(max(r, 0), 255) : 0u) << (8 * i);
+        }
+        *(uint32_t*)(D + (long long)py * lg.pitch) = word;
+    }
+}
+
 // ---- FAST per cell ----------------------------------------------------------------------
 // One workgroup (4 waves) per (cell, frame); the cell ROI (cell + 3 px each side) is staged
 // in LDS.  For threshold t = fastTh (and again at t = 7 when that finds <= 3 corners,
@@ -222,8 +240,6 @@ __device__ __forceinline__ void stage_rows_to_lds(uint32_t* __restrict__ dst, in
 //   nms     3x3 non-max suppression around each queued corner; neighbours outside the
 //           detection region, and non-corners, score 0 — cv::FAST on a cell-sized Mat
 // then the survivors are compacted in raster order as (score << 24) | (y << 12) | x.
-#define FAST_LCAP 2048  // corners queued for scoring
-#define FAST_QCAP 4096  // pre-filter survivors queued for the full test
 
 // cv::FAST corner test at threshold t: >= 9 contiguous circle pixels all > v+t or all < v-t.
 __device__ __forceinline__ bool fast_is_corner(const uint8_t* p, int TP, int t) {
@@ -304,113 +320,39 @@ __device__ __forceinline__ int fast_exact_strength(const uint8_t* p, int TP) {
     return max(A, B);
 }
 
-__global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ pyr, Geom g,
-                                                    const CellGeom* __restrict__ cells, uint32_t* __restrict__ cand,
-                                                    int* __restrict__ cellCount) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    __shared__ int s_nL, s_nQ, s_total;
-    const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+// The reference's `FAST(cellImage, keys, 7, true)` re-run of a cell that kept <= 3 corners at
+// fastTh (ORBextractor.cc:609-614), by the whole 256-thread workgroup: the cell ROI with its
+// 3 px ring is staged into LDS with dword loads, the strength plane at t = 7 computed, 3x3
+// strict NMS inside the detection region (out-of-region neighbours 0, as cv::FAST on the cell
+// Mat), survivors written in raster order as ((S - 1) << 24) | (y << 12) | x.  Returns the
+// survivor count (all threads).  smem: Sp (dwp x dh) | Fl (dwp x dh) | rowc | In.
+__device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int dw, int dh, int rx0, int ry0, int t,
+                               uint8_t* smem, uint32_t* __restrict__ out, int tid) {
     const int wave = tid >> 6, lane = tid & 63;
-    const CellGeom cg = cells[c];
-    int* outCount = cellCount + (long long)b * g.nCells + c;
-    const int dw = cg.hx - 6, dh = cg.hy - 6;
-    if (cg.skipped || dw <= 0 || dh <= 0) {
-        if (tid == 0) *outCount = 0;
-        return;
+    const int dwp = (dw + 3) & ~3, rw = dwp >> 2, nw = (dh * dwp) >> 2;
+    uint8_t* Sp = smem;
+    uint8_t* Fl = Sp + dh * dwp;
+    int* rowc = (int*)(Fl + dh * dwp);
+    uint8_t* In = (uint8_t*)(rowc + ((dh + 3) & ~3));
+    const int o = (int)((uintptr_t)(det - 3) & 3);  // dword alignment of the staged ROI
+    const int inW = (o + dw + 6 + 3) & ~3;
+    {
+        const uint32_t* src = (const uint32_t*)(det - 3 * (long long)pitch - 3 - o);
+        const int nwr = inW >> 2, pw = pitch >> 2;
+        for (int r = wave; r < dh + 6; r += 4)
+            for (int k = lane; k < nwr; k += 64) ((uint32_t*)In)[r * nwr + k] = src[(long long)r * pw + k];
+        for (int i = tid; i < nw; i += 256) ((uint32_t*)Fl)[i] = 0u;
     }
-    const LevelGeom& lg = g.lv[cg.level];
-    const uint8_t* roi =
-        pyr + lg.base + (long long)b * lg.fstride + (long long)(EDGE + cg.y0) * lg.pitch + EDGE + cg.x0;
-    const int sh = (int)((uintptr_t)roi & 3);
-    const uint32_t* src = (const uint32_t*)(roi - sh);
-    const int tw = (sh + cg.hx + 3) >> 2;  // words per tile row
-    const int TP = tw * 4;                 // tile row pitch in bytes
-    const int dwp = (dw + 3) & ~3;         // S / flag row pitch
-    const int nw = (dh * dwp) >> 2;        // words of the S (and flag) plane
-    uint32_t* tile = (uint32_t*)smem;
-    uint8_t* tb = smem + sh;                             // tb[y * TP + x] = ROI pixel (x, y)
-    uint8_t* Sb = smem + cg.hy * TP;                     // dh x dwp strengths (0 = not a corner)
-    uint8_t* Fl = Sb + dh * dwp;                         // dh x dwp keep flags
-    uint32_t* L = (uint32_t*)(Fl + dh * dwp);            // queued corners (y << 16 | x)
-    uint32_t* Q = L + FAST_LCAP;                         // queued pre-filter survivors
-    int* rowc = (int*)(Q + FAST_QCAP);                   // dh row counts / offsets
-    stage_rows_to_lds(tile, tw, src, lg.pitch >> 2, cg.hy, tw, tw, wave, lane);
-    int t = g.fastTh;
-    for (int pass = 0; pass < 2; ++pass) {
-        for (int i = tid; i < nw; i += 256) {
-            ((uint32_t*)Sb)[i] = 0u;
-            ((uint32_t*)Fl)[i] = 0u;
+    __syncthreads();
+    for (int yy = wave; yy < dh; yy += 4)
+        for (int xx = lane; xx < dw; xx += 64) {
+            const uint8_t* p = In + (yy + 3) * inW + xx + 3 + o;
+            Sp[yy * dwp + xx] = fast_is_corner(p, inW, t) ? (uint8_t)fast_exact_strength(p, inW) : (uint8_t)0;
         }
-        if (tid == 0) {
-            s_nL = 0;
-            s_nQ = 0;
-            s_total = 0;
-        }
-        __syncthreads();
-        // detect, stage 1: compass pre-filter over every pixel; survivors are queued in Q
-        // (overflow beyond FAST_QCAP is tested in place, in wave segments)
-        for (int yy = wave; yy < dh; yy += 4) {
-            const uint8_t* rowp = tb + (yy + 3) * TP + 3;
-            for (int xb = 0; xb < dw; xb += 64) {
-                const int xx = xb + lane;
-                const bool act = xx < dw;
-                const uint8_t* p = rowp + (act ? xx : 0);
-                const int v = p[0];
-                const int hi = v + t, lo = v - t;
-                const int q0 = p[3 * TP], q4 = p[3], q8 = p[-3 * TP], q12 = p[-3];
-                const int bm = (q0 > hi) | ((q4 > hi) << 1) | ((q8 > hi) << 2) | ((q12 > hi) << 3);
-                const int dm = (q0 < lo) | ((q4 < lo) << 1) | ((q8 < lo) << 2) | ((q12 < lo) << 3);
-                const bool pre = act && (((bm & ((bm >> 1) | (bm << 3))) | (dm & ((dm >> 1) | (dm << 3)))) & 0xF);
-                if (pre) {
-                    const int pos = atomicAdd(&s_nQ, 1);
-                    if (pos < FAST_QCAP) {
-                        Q[pos] = ((uint32_t)yy << 16) | (uint32_t)xx;
-                    } else if (fast_is_corner(p, TP, t)) {
-                        const int lp = atomicAdd(&s_nL, 1);
-                        if (lp < FAST_LCAP)
-                            L[lp] = ((uint32_t)yy << 16) | (uint32_t)xx;
-                        else
-                            Sb[yy * dwp + xx] = (uint8_t)fast_exact_strength(p, TP);
-                    }
-                }
-            }
-        }
-        __syncthreads();
-        // detect, stage 2: full 16-point 9-arc test on the queued pixels, all lanes busy
-        {
-            const int nq = min(s_nQ, FAST_QCAP);
-            for (int i = tid; i < nq; i += 256) {
-                const int yy = (int)(Q[i] >> 16), xx = (int)(Q[i] & 0xFFFF);
-                const uint8_t* p = tb + (yy + 3) * TP + 3 + xx;
-                if (fast_is_corner(p, TP, t)) {
-                    const int lp = atomicAdd(&s_nL, 1);
-                    if (lp < FAST_LCAP)
-                        L[lp] = Q[i];
-                    else
-                        Sb[yy * dwp + xx] = (uint8_t)fast_exact_strength(p, TP);
-                }
-            }
-        }
-        __syncthreads();
-        const int nQ = s_nL, nL = min(nQ, FAST_LCAP);
-        for (int i = tid; i < nL; i += 256) {
-            const int yy = (int)(L[i] >> 16), xx = (int)(L[i] & 0xFFFF);
-            Sb[yy * dwp + xx] = (uint8_t)fast_exact_strength(tb + (yy + 3) * TP + 3 + xx, TP);
-        }
-        __syncthreads();
-        // non-max suppression around every corner (all pixels when the queue overflowed)
-        int kept = 0;
-        const int nN = nQ > FAST_LCAP ? dh * dw : nL;
-        for (int i = tid; i < nN; i += 256) {
-            int yy, xx;
-            if (nQ > FAST_LCAP) {
-                yy = i / dw;
-                xx = i - yy * dw;
-            } else {
-                yy = (int)(L[i] >> 16);
-                xx = (int)(L[i] & 0xFFFF);
-            }
-            const int s0 = Sb[yy * dwp + xx];
+    __syncthreads();
+    for (int yy = wave; yy < dh; yy += 4)
+        for (int xx = lane; xx < dw; xx += 64) {
+            const int s0 = Sp[yy * dwp + xx];
             if (s0 <= t) continue;
             bool keep = true;
 #pragma unroll
@@ -419,34 +361,23 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
                 for (int dx = -1; dx <= 1; ++dx) {
                     if (dx == 0 && dy == 0) continue;
                     const int nx = xx + dx, ny = yy + dy;
-                    const int n = (nx >= 0 && nx < dw && ny >= 0 && ny < dh) ? Sb[ny * dwp + nx] : 0;
+                    const int n = (nx >= 0 && nx < dw && ny >= 0 && ny < dh) ? Sp[ny * dwp + nx] : 0;
                     keep = keep && (s0 - 1 > (n > t ? n - 1 : 0));
                 }
-            if (keep) {
-                Fl[yy * dwp + xx] = 1;
-                ++kept;
-            }
+            if (keep) Fl[yy * dwp + xx] = 1;
         }
-        if (kept) atomicAdd(&s_total, kept);
-        __syncthreads();
-        if (pass == 0 && s_total <= 3) {
-            t = 7;
-            __syncthreads();
-            continue;
-        }
-        break;
-    }
+    __syncthreads();
     // raster-order compaction from the flag plane: row counts, scan, write
     const uint32_t* Flw = (const uint32_t*)Fl;
-    const int rw = dwp >> 2;
     for (int yy = wave; yy < dh; yy += 4) {
         int cnt = 0;
         for (int w = lane; w < rw; w += 64) cnt += __popc(Flw[yy * rw + w]);
 #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+        for (int o2 = 32; o2 >= 1; o2 >>= 1) cnt += __shfl_xor(cnt, o2, 64);
         if (lane == 0) rowc[yy] = cnt;
     }
     __syncthreads();
+    __shared__ int s_total;
     if (wave == 0) {
         int carry = 0;
         for (int r0 = 0; r0 < dh; r0 += 64) {
@@ -454,41 +385,43 @@ __global__ void __launch_bounds__(256) k_fast_cells(const uint8_t* __restrict__ 
             const int v = r < dh ? rowc[r] : 0;
             int incl = v;
 #pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int nb = __shfl_up(incl, o, 64);
-                if (lane >= o) incl += nb;
+            for (int o2 = 1; o2 < 64; o2 <<= 1) {
+                const int nb = __shfl_up(incl, o2, 64);
+                if (lane >= o2) incl += nb;
             }
             if (r < dh) rowc[r] = carry + incl - v;
             carry += __shfl(incl, 63, 64);
         }
-        if (lane == 0) *outCount = carry;
+        if (lane == 0) s_total = carry;
     }
     __syncthreads();
-    uint32_t* out = cand + (long long)b * g.candPerFrame + cg.candOff;
     for (int yy = wave; yy < dh; yy += 4) {
         int off = rowc[yy];
-        const uint32_t ly = (uint32_t)(cg.y0 + 3 + yy) << 12;
+        const uint32_t ly = (uint32_t)(ry0 + yy) << 12;
         for (int w0 = 0; w0 < rw; w0 += 64) {
             const int w = w0 + lane;
             const uint32_t f = w < rw ? Flw[yy * rw + w] : 0u;
             const int n = __popc(f);
             int incl = n;
 #pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const int nb = __shfl_up(incl, o, 64);
-                if (lane >= o) incl += nb;
+            for (int o2 = 1; o2 < 64; o2 <<= 1) {
+                const int nb = __shfl_up(incl, o2, 64);
+                if (lane >= o2) incl += nb;
             }
             int pos = off + incl - n;
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if ((f >> (8 * j)) & 1u) {
-                    const int xx = 4 * w + j;
-                    const uint32_t sc = (uint32_t)(Sb[yy * dwp + xx] - 1);
-                    out[pos++] = (sc << 24) | ly | (uint32_t)(cg.x0 + 3 + xx);
+            for (int j2 = 0; j2 < 4; ++j2)
+                if ((f >> (8 * j2)) & 1u) {
+                    const int xx = 4 * w + j2;
+                    const uint32_t sc = (uint32_t)(Sp[yy * dwp + xx] - 1);
+                    out[pos++] = (sc << 24) | ly | (uint32_t)(rx0 + xx);
                 }
             off += __shfl(incl, 63, 64);
         }
     }
+    const int total = s_total;
+    __syncthreads();  // smem is reused by the caller
+    return total;
 }
 
 // ---- selection (retainBest replay) -------------------------------------------------------
@@ -496,32 +429,87 @@ struct ScoreGreater {  // KeypointResponseGreater on the packed FAST score
     ORB_HD bool operator()(uint32_t a, uint32_t b) const { return (a >> 24) > (b >> 24); }
 };
 
-// One wave per (level, frame).
-__global__ void __launch_bounds__(64) k_select(uint32_t* __restrict__ cand, const int* __restrict__ cellCount, Geom g,
-                                               const CellGeom* __restrict__ cells, uint32_t* __restrict__ lvlOut,
-                                               int* __restrict__ lvlCount) {
+// One workgroup per (level, frame).  In: each cell's NMS survivors at fastTh from k_level, in
+// arrival order, and their count.  (1) cells with <= 3 survivors are re-run at t = 7; (2) each
+// cell's survivors are put in raster order — the order cv::FAST returns them, which
+// retainBest's nth_element depends on; (3) nToRetain / redistribution (ORBextractor.cc:622-670);
+// (4) retainBest per cell, concatenation in cell order, retainBest to the level quota
+// (ORBextractor.cc:680-701) — exact libstdc++ nth_element replays.  Lists live in LDS when the
+// level's survivors fit (SELECT_CAP), otherwise in the frame's scratch area `cand2`.
+#define SELECT_CAP 6144
+__global__ void __launch_bounds__(256) k_select(const uint8_t* __restrict__ pyr, uint32_t* __restrict__ cand,
+                                                uint32_t* __restrict__ cand2, int* __restrict__ cellCount, Geom g,
+                                                const CellGeom* __restrict__ cells, uint32_t* __restrict__ lvlOut,
+                                                int* __restrict__ lvlCount) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ int s_cnt[ORB_MAX_CELLS_PER_LEVEL];
     __shared__ int s_ret[ORB_MAX_CELLS_PER_LEVEL];
     __shared__ int s_off[ORB_MAX_CELLS_PER_LEVEL + 1];
-    __shared__ uint32_t s_list[ORB_SELECT_LDS_CAP];
-    const int l = blockIdx.x, b = blockIdx.y, lane = threadIdx.x;
+    __shared__ int s_koff[ORB_MAX_CELLS_PER_LEVEL + 1];
+    __shared__ uint8_t s_skip[ORB_MAX_CELLS_PER_LEVEL];
+    __shared__ int s_fb[ORB_MAX_CELLS_PER_LEVEL + 1];  // cells to re-run at t = 7, count last
+    const int l = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const LevelGeom& lg = g.lv[l];
     const int nC = lg.rows * lg.cols;
     const CellGeom* lc = cells + lg.cell0;
     uint32_t* fcand = cand + (long long)b * g.candPerFrame;
-    for (int c = lane; c < nC; c += 64) s_cnt[c] = cellCount[(long long)b * g.nCells + lg.cell0 + c];
+    int* fcount = cellCount + (long long)b * g.nCells + lg.cell0;
+    if (tid < 64) {  // counts, skip flags, and the list of cells to re-run (ascending)
+        int nfb = 0;
+        for (int c0 = 0; c0 < nC; c0 += 64) {
+            const int c = c0 + lane;
+            bool fb = false;
+            if (c < nC) {
+                const CellGeom& cg = lc[c];
+                const int n = (cg.skipped || cg.hx <= 6 || cg.hy <= 6) ? 0 : min(fcount[c], cg.cap);
+                s_cnt[c] = n;
+                s_skip[c] = (uint8_t)cg.skipped;
+                fb = !cg.skipped && n <= 3;
+            }
+            const uint64_t m = __ballot(fb);
+            if (fb) s_fb[nfb + __popcll(m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))))] = c;
+            nfb += __popcll(m);
+        }
+        if (lane == 0) s_fb[ORB_MAX_CELLS_PER_LEVEL] = nfb;
+    }
     __syncthreads();
-    if (lane == 0) {
-        // nToRetain / nToDistribute / bNoMore bookkeeping (ORBextractor.cc:622-670)
+    // (1) FAST(cellImage, keys, 7, true) where a cell kept <= 3 (a skipped cell is `continue`d)
+    {
+        const int nfb = s_fb[ORB_MAX_CELLS_PER_LEVEL];
+        for (int f = 0; f < nfb; ++f) {
+            const int c = s_fb[f];
+            const CellGeom cg = lc[c];
+            const int dw = cg.hx - 6, dh = cg.hy - 6;
+            int n = 0;
+            if (dw > 0 && dh > 0) {
+                const uint8_t* det = pyr + lg.base + (long long)b * lg.fstride +
+                                     (long long)(EDGE + cg.y0 + 3) * lg.pitch + EDGE + cg.x0 + 3;
+                n = cell_fast_rerun(det, lg.pitch, dw, dh, cg.x0 + 3, cg.y0 + 3, 7, smem, fcand + cg.candOff, tid);
+            }
+            if (tid == 0) {
+                s_cnt[c] = n;
+                fcount[c] = n;
+            }
+            __syncthreads();
+        }
+    }
+    if (tid == 0) {
+        int s = 0;
+        for (int c = 0; c < nC; ++c) {
+            s_off[c] = s;
+            s += s_cnt[c];
+        }
+        s_off[nC] = s;
+        // (3) nToRetain / nToDistribute / bNoMore bookkeeping (ORBextractor.cc:622-670)
         const int nfc = lg.nfc;
         int nNoMore = 0, nToDistribute = 0;
         unsigned long long noMore[(ORB_MAX_CELLS_PER_LEVEL + 63) / 64] = {};
         for (int c = 0; c < nC; ++c) {
-            if (lc[c].skipped) {
+            if (s_skip[c]) {
                 s_ret[c] = 0;
                 continue;
             }
-            int nKeys = s_cnt[c];
+            const int nKeys = s_cnt[c];
             if (nKeys > nfc) {
                 s_ret[c] = nfc;
             } else {
@@ -532,11 +520,11 @@ __global__ void __launch_bounds__(64) k_select(uint32_t* __restrict__ cand, cons
             }
         }
         while (nToDistribute > 0 && nNoMore < nC) {
-            int nNew = nfc + (int)ceilf((float)nToDistribute / (nC - nNoMore));
+            const int nNew = nfc + (int)ceilf((float)nToDistribute / (nC - nNoMore));
             nToDistribute = 0;
             for (int c = 0; c < nC; ++c) {
                 if (noMore[c >> 6] & (1ull << (c & 63))) continue;
-                int tot = lc[c].skipped ? 0 : s_cnt[c];
+                const int tot = s_skip[c] ? 0 : s_cnt[c];
                 if (tot > nNew) {
                     s_ret[c] = nNew;
                 } else {
@@ -549,53 +537,75 @@ __global__ void __launch_bounds__(64) k_select(uint32_t* __restrict__ cand, cons
         }
     }
     __syncthreads();
-    ScoreGreater comp;
-    for (int c = lane; c < nC; c += 64) {
-        int n = lc[c].skipped ? 0 : s_cnt[c];
-        s_cnt[c] = orbsel::retain_best(fcand + lc[c].candOff, n, s_ret[c], comp);
+    const int M = s_off[nC];
+    const bool inLds = M <= SELECT_CAP;
+    uint32_t* raw = (uint32_t*)smem;                                      // arrival order
+    uint32_t* srt = inLds ? raw + SELECT_CAP : cand2 + (long long)b * g.candPerFrame;  // raster order
+    const uint32_t* srcOf = inLds ? raw : fcand;
+    if (inLds) {
+        for (int c = wave; c < nC; c += 4)
+            for (int k = lane; k < s_cnt[c]; k += 64) raw[s_off[c] + k] = fcand[lc[c].candOff + k];
+        __syncthreads();
+    }
+    // (2) rank sort of each cell by position (positions are unique)
+    for (int c = wave; c < nC; c += 4) {
+        const int n = s_cnt[c];
+        const uint32_t* seg = srcOf + (inLds ? s_off[c] : lc[c].candOff);
+        uint32_t* dst = srt + (inLds ? s_off[c] : lc[c].candOff);
+        for (int i = lane; i < n; i += 64) {
+            const uint32_t e = seg[i], key = e & 0xFFFFFFu;
+            int r = 0;
+            for (int j2 = 0; j2 < n; ++j2) r += (seg[j2] & 0xFFFFFFu) < key;
+            dst[r] = e;
+        }
     }
     __syncthreads();
-    if (lane == 0) {
+    // (4) retainBest per cell, then the level list in cell order, then retainBest to the quota
+    ScoreGreater comp;
+    for (int c = tid; c < nC; c += 256) {
+        uint32_t* seg = srt + (inLds ? s_off[c] : lc[c].candOff);
+        s_cnt[c] = orbsel::retain_best(seg, s_cnt[c], s_ret[c], comp);
+    }
+    __syncthreads();
+    if (tid == 0) {
         int s = 0;
         for (int c = 0; c < nC; ++c) {
-            s_off[c] = s;
+            s_koff[c] = s;
             s += s_cnt[c];
         }
-        s_off[nC] = s;
+        s_koff[nC] = s;
     }
     __syncthreads();
-    const int M = s_off[nC];
+    const int K = s_koff[nC];
     uint32_t* list;
-    if (M <= ORB_SELECT_LDS_CAP) {
-        for (int c = 0; c < nC; ++c) {
-            const uint32_t* src = fcand + lc[c].candOff;
-            for (int k = lane; k < s_cnt[c]; k += 64) s_list[s_off[c] + k] = src[k];
-        }
-        list = s_list;
-    } else {  // sequential in-place compaction (dest <= src, ascending) into the level's area
-        list = fcand + lc[0].candOff;
-        if (lane == 0)
+    if (inLds) {  // kept prefixes of srt -> raw (disjoint regions)
+        for (int c = wave; c < nC; c += 4)
+            for (int k = lane; k < s_cnt[c]; k += 64) raw[s_koff[c] + k] = srt[s_off[c] + k];
+        list = raw;
+    } else {  // sequential in-place compaction (dest <= src, ascending) in cand2's level area
+        list = srt + lc[0].candOff;
+        if (tid == 0)
             for (int c = 0; c < nC; ++c) {
-                const uint32_t* src = fcand + lc[c].candOff;
-                for (int k = 0; k < s_cnt[c]; ++k) list[s_off[c] + k] = src[k];
+                const uint32_t* src = srt + lc[c].candOff;
+                for (int k = 0; k < s_cnt[c]; ++k) list[s_koff[c] + k] = src[k];
             }
     }
     __syncthreads();
-    int keep = M;
-    if (M > lg.nDesired) {
+    int keep = K;
+    if (K > lg.nDesired) {
         keep = lg.nDesired;
-        if (lane == 0) orbsel::retain_best(list, M, lg.nDesired, comp);
+        if (tid == 0) orbsel::retain_best(list, K, lg.nDesired, comp);
     }
     __syncthreads();
     uint32_t* out = lvlOut + (long long)b * g.kpCap + lg.kpBase;
-    for (int k = lane; k < keep; k += 64) out[k] = list[k];
-    if (lane == 0) lvlCount[(long long)b * g.L + l] = keep;
+    for (int k = tid; k < keep; k += 256) out[k] = list[k];
+    if (tid == 0) lvlCount[(long long)b * g.L + l] = keep;
 }
 
 // ---- descriptor image: GaussianBlur(level ROI, 7x7, sigma 2) in place ---------------------
 // The reference blurs the level ROI in place right before its descriptors
 // (ORBextractor.cc:760): samples inside the ROI read the blur, samples in the 16-px padding
-// read the un-blurred reflect-101 border (rBRIEF reaches 2 px into it).  k_blur materialises
+// read the un-blurred reflect-101 border (rBRIEF reaches 2 px into it).  k_level materialises
 // exactly that image over level coordinates [-3, w+3) x [-3, h+3) in a buffer laid out like
 // the pyramid.  Fixed-point taps (18,34,49,55,49,34,18)/256 per axis:
 // T = sum_j k_j sum_i k_i P; columns x < 4*floor(w/4) round T/65536 half-to-even (the SSE2
@@ -610,70 +620,258 @@ struct BlurTile {
 
 __device__ __forceinline__ int byte_of(uint32_t w, int k) { return (int)((w >> (8 * k)) & 0xFFu); }
 
-__global__ void __launch_bounds__(256) k_blur(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur, Geom g,
-                                              const BlurTile* __restrict__ tiles) {
-    __shared__ __attribute__((aligned(16))) uint32_t s_in[(BLUR_TH + 6) * BLUR_IW];
+#define LVL_FQ 512  // per-wave FAST queue capacity (u16 entries)
+
+// Full 9-arc test + exact strength on a wave's pre-filter queue (pq, qn entries of
+// (row << 8 | col) in the wave's rows of the staged tile); corners are appended to the
+// (frame, level) list as (S << 24) | (y << 12) | x.  Rare enough to live out of line.
+#define LVL_SPW 264  // LDS strength-plane row pitch (bytes): tile columns -4 .. 259
+
+// Full 9-arc test + exact strength on a wave's FAST queue (pq, qn entries of
+// ((row + 1) << 9) | (col + 1), tile-relative, row in [-1, TH], col in [-1, 256]); corners
+// store S into the tile's strength plane Sp (row + 1, col + 4).  Out of line: runs once per
+// ~256 queued pixels of a wave.
+__device__ __attribute__((noinline)) void level_drain(const uint8_t* inb, uint16_t* pq, uint16_t* cq, int qn, int ft,
+                                                      uint8_t* Sp, int lane) {
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const int TP = BLUR_IW * 4;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    int cn = 0;
+    for (int i0 = 0; i0 < qn; i0 += 64) {
+        const int i = i0 + lane;
+        bool corner = false;
+        uint16_t e = 0;
+        if (i < qn) {
+            e = pq[i];
+            const uint8_t* p = inb + ((e >> 9) + 3) * TP + (e & 511) + 3;
+            corner = fast_is_corner(p, TP, ft);
+        }
+        const uint64_t m = __ballot(corner);
+        if (corner) cq[cn + __popcll(m & below)] = e;
+        cn += __popcll(m);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    for (int i = lane; i < cn; i += 64) {
+        const uint16_t e = cq[i];
+        const uint8_t* p = inb + ((e >> 9) + 3) * TP + (e & 511) + 3;
+        Sp[(e >> 9) * LVL_SPW + (e & 511) + 3] = (uint8_t)fast_exact_strength(p, TP);
+    }
+}
+
+// One tile of one level, four waves of BLUR_RW rows:
+//   (1) the descriptor image rows of the wave (blur);
+//   (2) FAST at fastTh inside the detection region [16, w-16) x [16, h-16): compass pre-filter
+//       on 4 px per lane from the dword rings the blur already holds, survivors queued per
+//       wave; the full 9-arc test and the exact strength S run on the queue with all lanes
+//       busy (level_drain) and land in an LDS strength plane, which also holds the tile's 1-px
+//       halo ring (queued without pre-filter);
+//   (3) after one barrier, the per-cell 3x3 NMS of cv::FAST(cellImage, fastTh, true)
+//       (ORBextractor.cc:599-607) from the plane: a corner survives iff S-1 beats the score of
+//       each 8-neighbour inside its cell's detection area (S-1 for a corner, else 0).
+//       Survivors are appended to their cell's candidate slots as ((S-1) << 24) | (y << 12) | x;
+//       cells tile the detection region, so (cell row, col) = ((y-16)/cellH, (x-16)/cellW).
+//       k_select restores raster order.
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+k_level(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur, Geom g, const BlurTile* __restrict__ tiles,
+        const CellGeom* __restrict__ cells, uint32_t* __restrict__ cand, int* __restrict__ cellCount) {
+    __shared__ __attribute__((aligned(16))) uint32_t s_in[(BLUR_TH + 8) * BLUR_IW];
+    __shared__ __attribute__((aligned(16))) uint8_t s_S[(BLUR_TH + 2) * LVL_SPW];
+    __shared__ uint16_t s_pq[4][LVL_FQ];
+    __shared__ uint16_t s_cq[4][LVL_FQ];
     const BlurTile t = tiles[blockIdx.x];
     const int b = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const LevelGeom& lg = g.lv[t.level];
     const uint8_t* src = pyr + lg.base + (long long)b * lg.fstride;
     uint8_t* dst = blur + lg.base + (long long)b * lg.fstride;
-    // input rows y0-3 .. y0+TH+2, columns x0-4 .. x0+259 (padded +16: dword aligned).  Rows
-    // past the padded buffer are only needed by rows that are never written: not loaded.
-    const int py0 = t.y0 - 3 + EDGE, px0 = t.x0 - 4 + EDGE;
-    const int rows = min(BLUR_TH + 6, lg.ph - py0);
+    // input rows y0-4 .. y0+TH+3 (blur: +-3; FAST ring of a halo pixel: +-4), columns
+    // x0-4 .. x0+259 (padded +16: dword aligned).  Rows past the padded buffer are only needed
+    // by rows that are never written: not loaded.
+    const int py0 = t.y0 - 4 + EDGE, px0 = t.x0 - 4 + EDGE;
+    const int rows = min(BLUR_TH + 8, lg.ph - py0);
     const int spw = lg.pitch >> 2;
     stage_rows_to_lds(s_in, BLUR_IW, (const uint32_t*)(src + (long long)py0 * lg.pitch + px0), spw, rows, BLUR_IW,
                       spw - (px0 >> 2), wave, lane);
+    for (int i = tid; i < (BLUR_TH + 2) * LVL_SPW / 4; i += 256) ((uint32_t*)s_S)[i] = 0u;
     __syncthreads();
-    const int x = t.x0 + 4 * lane;  // first of this lane's 4 output columns
-    if (x >= lg.w + 4) return;
-    const int k0 = g.taps[0], k1 = g.taps[1], k2 = g.taps[2], k3 = g.taps[3];
-    const uint32_t* in = s_in + (wave * BLUR_RW) * BLUR_IW + lane;
-    int R[7][4];
-    uint32_t C[7];  // raw centre dword of each ring row
-#pragma unroll
-    for (int r = 0; r < BLUR_RW + 6; ++r) {
-        const uint32_t d0 = in[r * BLUR_IW], d1 = in[r * BLUR_IW + 1], d2 = in[r * BLUR_IW + 2];
-        int B[12];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            B[k] = byte_of(d0, k);
-            B[4 + k] = byte_of(d1, k);
-            B[8 + k] = byte_of(d2, k);
+    const uint8_t* inb = (const uint8_t*)s_in;
+    const int ft = g.fastTh;
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint16_t* pq = s_pq[wave];
+    uint16_t* cq = s_cq[wave];
+    int qn = 0;
+    {  // halo ring of the strength plane: row -1 (wave 0), row TH (wave 3), columns -1 and 256
+        auto inDet = [&](int rt, int ct) {
+            const int X = t.x0 + ct, Y = t.y0 + rt;
+            return X >= EDGE && X < lg.detX1 && Y >= EDGE && Y < lg.detY1;
+        };
+        auto push = [&](bool v, int rt, int ct) {
+            const uint64_t m = __ballot(v);
+            if (v) pq[qn + __popcll(m & below)] = (uint16_t)(((rt + 1) << 9) | (ct + 1));
+            qn += __popcll(m);
+        };
+        if (wave == 0 || wave == 3) {
+            const int rt = wave == 0 ? -1 : BLUR_TH;
+            for (int c0 = -1; c0 <= BLUR_TW; c0 += 64) {
+                const int ct = c0 + lane;
+                push(ct <= BLUR_TW && inDet(rt, ct), rt, ct);
+            }
         }
+        {
+            const int rt = wave * BLUR_RW + (lane & 15), ct = (lane & 16) ? BLUR_TW : -1;
+            push(lane < 32 && inDet(rt, ct), rt, ct);
+        }
+        if (qn > LVL_FQ - 256) {
+            level_drain(inb, pq, cq, qn, ft, s_S, lane);
+            qn = 0;
+        }
+    }
+    const int x = t.x0 + 4 * lane;  // first of this lane's 4 output columns
+    const bool colLive = x < lg.w + 4;
+    const int k0 = g.taps[0], k1 = g.taps[1], k2 = g.taps[2], k3 = g.taps[3];
+    const uint32_t* in = s_in + (wave * BLUR_RW + 1) * BLUR_IW + lane;
+    int R[7][4];
+    uint32_t C[7], A[7], Z[7];  // dwords of each ring row: centre (x..x+3), left (x-4..x-1), right (x+4..x+7)
+    bool done = false;
+    for (int r0 = 0; r0 < BLUR_RW + 6 && !done; r0 += 7) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-            R[r % 7][j] = k0 * B[4 + j] + k1 * (B[3 + j] + B[5 + j]) + k2 * (B[2 + j] + B[6 + j]) +
-                          k3 * (B[1 + j] + B[7 + j]);
-        C[r % 7] = d1;
-        if (r < 6) continue;
-        const int y = t.y0 + wave * BLUR_RW + (r - 6);  // output row; ring row (r - 3) is its centre
-        if (y >= lg.h + 3) break;
-        const bool rowIn = y >= 0 && y < lg.h;
-        const uint32_t craw = C[(r - 3) % 7];
-        uint32_t word = 0;
+        for (int k = 0; k < 7; ++k) {  // ring slot of row r = r0 + k is k (r0 is a multiple of 7)
+            const int r = r0 + k;
+            if (done || r >= BLUR_RW + 6) break;
+            const uint32_t d0 = in[r * BLUR_IW], d1 = in[r * BLUR_IW + 1], d2 = in[r * BLUR_IW + 2];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int b1 = byte_of(j < 3 ? d0 : d1, (j + 1) & 3), b2 = byte_of(j < 2 ? d0 : d1, (j + 2) & 3);
+                const int b3 = byte_of(j < 1 ? d0 : d1, (j + 3) & 3), b4 = byte_of(d1, j);
+                const int b5 = byte_of(j < 3 ? d1 : d2, (j + 1) & 3), b6 = byte_of(j < 2 ? d1 : d2, (j + 2) & 3);
+                const int b7 = byte_of(j < 1 ? d1 : d2, (j + 3) & 3);
+                R[k][j] = k0 * b4 + k1 * (b3 + b5) + k2 * (b2 + b6) + k3 * (b1 + b7);
+            }
+            C[k] = d1;
+            A[k] = d0;
+            Z[k] = d2;
+            if (r < 6) continue;
+            const int y = t.y0 + wave * BLUR_RW + (r - 6);  // output row; ring slot (k+4)%7 is its centre
+            if (y >= lg.h + 3) {
+                done = true;
+                break;
+            }
+            const int kc = (k + 4) % 7, km1 = (k + 3) % 7, kp1 = (k + 5) % 7, km2 = (k + 2) % 7, kp2 = (k + 6) % 7,
+                      km3 = (k + 1) % 7;
+            if (colLive) {
+                const bool rowIn = y >= 0 && y < lg.h;
+                const uint32_t craw = C[kc];
+                uint32_t word = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int xj = x + j;
+                    int v;
+                    if (rowIn && xj >= 0 && xj < lg.w) {
+                        const int T = k0 * R[kc][j] + k1 * (R[km1][j] + R[kp1][j]) + k2 * (R[km2][j] + R[kp2][j]) +
+                                      k3 * (R[km3][j] + R[k][j]);
+                        v = xj < lg.xsimd_blur ? (T + 32767 + ((T >> 16) & 1)) >> 16 : (T + 32768) >> 16;
+                        v = min(v, 255);
+                    } else {
+                        v = byte_of(craw, j);  // outside the ROI: the un-blurred padding
+                    }
+                    word |= (uint32_t)v << (8 * j);
+                }
+                *(uint32_t*)(dst + (long long)(y + EDGE) * lg.pitch + (x + EDGE)) = word;
+            }
+            // FAST pre-filter for the row (wave-uniform row test)
+            if (y >= EDGE && y < lg.detY1) {
+                const uint32_t cc = C[kc], cd = C[k], cu = C[km3];
+                const uint32_t a4 = __builtin_amdgcn_alignbyte(Z[kc], cc, 3);   // x+3 .. x+6
+                const uint32_t a12 = __builtin_amdgcn_alignbyte(cc, A[kc], 1);  // x-3 .. x
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int xj = x + j;
+                    const int v = byte_of(cc, j), hi = v + ft, lo = v - ft;
+                    const int q0 = byte_of(cd, j), q4 = byte_of(a4, j), q8 = byte_of(cu, j), q12 = byte_of(a12, j);
+                    const int bm = (q0 > hi) | ((q4 > hi) << 1) | ((q8 > hi) << 2) | ((q12 > hi) << 3);
+                    const int dm = (q0 < lo) | ((q4 < lo) << 1) | ((q8 < lo) << 2) | ((q12 < lo) << 3);
+                    const bool pre = xj >= EDGE && xj < lg.detX1 &&
+                                     (((bm & ((bm >> 1) | (bm << 3))) | (dm & ((dm >> 1) | (dm << 3)))) & 0xF);
+                    const uint64_t m = __ballot(pre);
+                    if (pre) pq[qn + __popcll(m & below)] = (uint16_t)(((wave * BLUR_RW + r - 5) << 9) | (4 * lane + j + 1));
+                    qn += __popcll(m);
+                }
+                if (qn > LVL_FQ - 256) {
+                    level_drain(inb, pq, cq, qn, ft, s_S, lane);
+                    qn = 0;
+                }
+            }
+        }
+    }
+    if (qn) level_drain(inb, pq, cq, qn, ft, s_S, lane);
+    __syncthreads();
+    // (3) in-cell NMS over the wave's rows of the plane, 4 columns per lane.  Cell (i, j) has
+    // the detection area [16 + j*cellW, j == cols-1 ? w-16 : 16 + (j+1)*cellW) in x (likewise
+    // in y), ORBextractor.cc:572-597.
+    auto cellRange = [](int v, int n, int cs, int lim, int& k, int& lo, int& hi) {
+        k = (v - EDGE) / cs;
+        lo = EDGE + k * cs;
+        hi = k == n - 1 ? lim - EDGE : lo + cs;
+    };
+    const CellGeom* lc = cells + lg.cell0;
+    int* fcount = cellCount + (long long)b * g.nCells + lg.cell0;
+    uint32_t* fcand = cand + (long long)b * g.candPerFrame;
+    auto emit = [&](int n) {  // all lanes in parallel
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        for (int k = lane; k < n; k += 64) {
+            const uint16_t e = cq[k];
+            const int rte = e >> 9, ct = e & 511;
+            const int X = t.x0 + ct, Ye = t.y0 + rte;
+            const int c = ((Ye - EDGE) / lg.cellH) * lg.cols + (X - EDGE) / lg.cellW;
+            const int S = s_S[(rte + 1) * LVL_SPW + ct + 4];
+            const int cap = lc[c].cap, off = lc[c].candOff;
+            const int pos = atomicAdd(fcount + c, 1);
+            if (pos < cap) fcand[off + pos] = ((uint32_t)(S - 1) << 24) | ((uint32_t)Ye << 12) | (uint32_t)X;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    };
+    int cjs[4], xlo[4], xhi[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cellRange(max(t.x0 + 4 * lane + j, EDGE), lg.cols, lg.cellW, lg.w, cjs[j], xlo[j], xhi[j]);
+    int cn = 0;
+    for (int i = 0; i < BLUR_RW; ++i) {
+        const int rt = wave * BLUR_RW + i;
+        const int Y = t.y0 + rt;
+        if (Y < EDGE || Y >= lg.detY1) continue;  // wave-uniform
+        int ci, ylo, yhi;
+        cellRange(Y, lg.rows, lg.cellH, lg.h, ci, ylo, yhi);
+        const uint32_t w4 = *(const uint32_t*)(s_S + (rt + 1) * LVL_SPW + 4 + 4 * lane);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const int xj = x + j;
-            int v;
-            if (rowIn && xj >= 0 && xj < lg.w) {
-                const int T = k0 * R[(r - 3) % 7][j] + k1 * (R[(r - 4) % 7][j] + R[(r - 2) % 7][j]) +
-                              k2 * (R[(r - 5) % 7][j] + R[(r - 1) % 7][j]) + k3 * (R[(r - 6) % 7][j] + R[r % 7][j]);
-                v = xj < lg.xsimd_blur ? (T + 32767 + ((T >> 16) & 1)) >> 16 : (T + 32768) >> 16;
-                v = min(v, 255);
-            } else {
-                v = byte_of(craw, j);  // outside the ROI: the un-blurred padding
+            const int S = (w4 >> (8 * j)) & 0xFF;
+            bool keep = S != 0 && ci < lg.rows && cjs[j] < lg.cols;
+            if (keep) {
+                const int ct = 4 * lane + j, X = t.x0 + ct;
+                const uint8_t* sp = s_S + (rt + 1) * LVL_SPW + ct + 4;
+#pragma unroll
+                for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+                    for (int dx = -1; dx <= 1; ++dx) {
+                        if (dx == 0 && dy == 0) continue;
+                        const bool inCell = X + dx >= xlo[j] && X + dx < xhi[j] && Y + dy >= ylo && Y + dy < yhi;
+                        const int n = inCell ? sp[dy * LVL_SPW + dx] : 0;
+                        keep = keep && (S - 1 > (n ? n - 1 : 0));
+                    }
             }
-            word |= (uint32_t)v << (8 * j);
+            const uint64_t m = __ballot(keep);
+            if (keep) cq[cn + __popcll(m & below)] = (uint16_t)((rt << 9) | (4 * lane + j));
+            cn += __popcll(m);
         }
-        *(uint32_t*)(dst + (long long)(y + EDGE) * lg.pitch + (x + EDGE)) = word;
+        if (cn > LVL_FQ - 256) {
+            emit(cn);
+            cn = 0;
+        }
     }
+    if (cn) emit(cn);
 }
 
 // ---- orientation + descriptor -------------------------------------------------------------
 // One wave per keypoint.  IC angle on the raw level (31x31 disc staged in LDS with dword
-// loads); the 512 rBRIEF samples read the descriptor image built by k_blur.
+// loads); the 512 rBRIEF samples read the descriptor image built by k_level.
 #define IC_P 36  // LDS pitch of the 31-row IC patch
 
 __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__ pyr,
@@ -1123,7 +1321,8 @@ struct orb_extractor {
     Geom g{};
     std::vector<CellGeom> cells;
     std::vector<int> rtab;
-    size_t cellLds = 0;
+    size_t cellLds = 0, selectLds = 0;
+    size_t resizeLds[ORB_MAX_LEVELS] = {};
     // device workspace
     uint8_t* d_pyr = nullptr;
     uint8_t* d_blur = nullptr;
@@ -1131,12 +1330,13 @@ struct orb_extractor {
     int nTiles = 0;
     uint32_t* d_cand = nullptr;
     int* d_cellCount = nullptr;
+    uint32_t* d_cand2 = nullptr;  // k_select scratch when a level's survivors exceed its LDS
     uint32_t* d_lvl = nullptr;
     int* d_lvlCount = nullptr;
     int* d_rtab = nullptr;
     CellGeom* d_cells = nullptr;
     // per-stage HIP-event timing (orb_profile_*): stage k brackets its kernel(s) on the launch stream
-    static constexpr int kStages = 6;
+    static constexpr int kStages = 5;
     bool prof = false;
     std::vector<hipEvent_t> evPool;  // 2 per stage per launch, recycled after each read
     std::vector<std::pair<int, int>> evPending;  // (stage, index of the start event)
@@ -1162,6 +1362,7 @@ struct orb_extractor {
         hipFree(d_tiles);
         hipFree(d_cand);
         hipFree(d_cellCount);
+        hipFree(d_cand2);
         hipFree(d_lvl);
         hipFree(d_lvlCount);
         hipFree(d_rtab);
@@ -1176,6 +1377,7 @@ struct orb_extractor {
         nTiles = 0;
         d_cand = nullptr;
         d_cellCount = nullptr;
+        d_cand2 = nullptr;
         d_lvl = nullptr;
         d_lvlCount = nullptr;
         d_rtab = nullptr;
@@ -1221,7 +1423,6 @@ struct orb_extractor {
         Geom G{};
         G.L = nlevels;
         G.fastTh = std::min(std::max(fastTh, 0), 255);
-        G.tmin = std::min(G.fastTh, 7);
         G.scoreType = scoreType;
         int k7[7];
         gaussian_taps7(k7);
@@ -1270,6 +1471,11 @@ struct orb_extractor {
             lg.rows = levelRows;
             lg.cols = levelCols;
             lg.nfc = (int)std::ceil((float)nD / nCells);
+            lg.cellW = cellW;
+            lg.cellH = cellH;
+            lg.detX1 = std::max(maxBX, levelCols > 1 ? 16 + (levelCols - 1) * cellW : 0);
+            lg.detY1 = std::max(maxBY, levelRows > 1 ? 16 + (levelRows - 1) * cellH : 0);
+            if (cellW <= 0 || cellH <= 0) return set_err(ORB_ENOTSUP, "empty cell size");
             lg.cell0 = (int)cl.size();
             std::vector<int> iniXCol(levelCols, 0);
             float hY = cellH + 6;
@@ -1308,9 +1514,9 @@ struct orb_extractor {
                             int dw = c.hx - 6, dh = c.hy - 6;
                             c.cap = (dw > 0 && dh > 0) ? ((dw + 1) / 2) * ((dh + 1) / 2) : 0;
                             const size_t dwp = (size_t)((std::max(dw, 0) + 3) & ~3);
-                            size_t lds = (size_t)(((c.hx + 3 + 3) >> 2) * 4) * c.hy +
-                                         2 * dwp * std::max(dh, 0) + 4 * (FAST_LCAP + FAST_QCAP) +
-                                         4 * (size_t)std::max(dh, 0) + 16;
+                            const size_t inW = (size_t)((3 + std::max(dw, 0) + 6 + 3) & ~3);
+                            size_t lds = 2 * dwp * std::max(dh, 0) + 4 * (size_t)((std::max(dh, 0) + 3) & ~3) +
+                                         inW * (std::max(dh, 0) + 6) + 16;
                             cellLds = std::max(cellLds, lds);
                         }
                     }
@@ -1320,7 +1526,8 @@ struct orb_extractor {
                 }
             }
         }
-        if (cellLds > 150 * 1024) return set_err(ORB_ENOTSUP, "FAST cell larger than the LDS budget");
+        selectLds = std::max(cellLds, (size_t)2 * SELECT_CAP * 4);
+        if (selectLds > 150 * 1024) return set_err(ORB_ENOTSUP, "FAST cell larger than the LDS budget");
         // resize tables, l >= 1
         for (int l = 1; l < nlevels; ++l) {
             LevelGeom& lg = G.lv[l];
@@ -1365,6 +1572,34 @@ struct orb_extractor {
             rt.insert(rt.end(), alpha.begin(), alpha.end());
             rt.insert(rt.end(), yofs.begin(), yofs.end());
             rt.insert(rt.end(), beta.begin(), beta.end());
+            // source rectangle of every RZ_TW x RZ_TH tile of the padded level (k_pyr_resize)
+            const int tx = (lg.pitch + RZ_TW - 1) / RZ_TW, ty = (lg.ph + RZ_TH - 1) / RZ_TH;
+            lg.rtile = (int)rt.size();
+            size_t lds = 0;
+            for (int y = 0; y < ty; ++y)
+                for (int x = 0; x < tx; ++x) {
+                    int c0 = INT32_MAX, c1 = -1, r0 = INT32_MAX, r1 = -1;
+                    for (int px = x * RZ_TW; px < std::min((x + 1) * RZ_TW, lg.pitch); ++px) {
+                        const int lx = orbdev::reflect101(std::min(px, dw + 31) - 16, dw);
+                        const int sx = xofs[lx];
+                        const int sx1 = (lx < xmax && (alpha[lx] >> 16) != 0) ? sx + 1 : sx;
+                        c0 = std::min(c0, sx);
+                        c1 = std::max(c1, sx1);
+                    }
+                    for (int py = y * RZ_TH; py < std::min((y + 1) * RZ_TH, lg.ph); ++py) {
+                        const int ly = orbdev::reflect101(py - 16, dh);
+                        r0 = std::min(r0, std::min(std::max(yofs[ly], 0), sh - 1));
+                        r1 = std::max(r1, std::min(std::max(yofs[ly] + 1, 0), sh - 1));
+                    }
+                    const int cs = c0 & ~3, words = ((c1 - cs) >> 2) + 1, nr = r1 - r0 + 1;
+                    rt.push_back(cs);
+                    rt.push_back(words);
+                    rt.push_back(r0);
+                    rt.push_back(nr);
+                    lds = std::max(lds, (size_t)words * 4 * nr);
+                }
+            if (lds > 96 * 1024) return set_err(ORB_ENOTSUP, "scale factor too large for the resize tile");
+            resizeLds[l] = lds;
         }
         G.nCells = (int)cl.size();
         G.candPerFrame = cand;
@@ -1381,6 +1616,7 @@ struct orb_extractor {
         nTiles = (int)tl.size();
         HIP_TRY(hipMalloc(&d_cand, (size_t)std::max(cand, 1) * maxBatch * 4));
         HIP_TRY(hipMalloc(&d_cellCount, (size_t)G.nCells * maxBatch * 4));
+        HIP_TRY(hipMalloc(&d_cand2, (size_t)std::max(cand, 1) * maxBatch * 4));
         HIP_TRY(hipMalloc(&d_lvl, (size_t)std::max(kpCap, 1) * maxBatch * 4));
         HIP_TRY(hipMalloc(&d_lvlCount, (size_t)nlevels * maxBatch * 4));
         HIP_TRY(hipMalloc(&d_rtab, std::max<size_t>(rt.size(), 1) * 4));
@@ -1453,22 +1689,20 @@ struct orb_extractor {
         stage_begin(1, st);
         for (int l = 1; l < nlevels; ++l) {
             const LevelGeom& lg = g.lv[l];
-            dim3 grid((lg.pitch / 4 + 63) / 64, (lg.ph + 4 * PYR_RW - 1) / (4 * PYR_RW), B);
-            hipLaunchKernelGGL(k_pyr_resize, grid, dim3(64, 4), 0, st, d_pyr, d_rtab, g, l);
+            dim3 grid((lg.pitch + RZ_TW - 1) / RZ_TW, (lg.ph + RZ_TH - 1) / RZ_TH, B);
+            hipLaunchKernelGGL(k_pyr_resize, grid, dim3(256), resizeLds[l], st, d_pyr, d_rtab, g, l);
         }
         stage_end(st);
         stage_begin(2, st);
-        hipLaunchKernelGGL(k_fast_cells, dim3(g.nCells, B), dim3(256), cellLds, st, d_pyr, g, d_cells, d_cand,
+        HIP_TRY(hipMemsetAsync(d_cellCount, 0, (size_t)g.nCells * B * 4, st));
+        hipLaunchKernelGGL(k_level, dim3(nTiles, B), dim3(256), 0, st, d_pyr, d_blur, g, d_tiles, d_cells, d_cand,
                            d_cellCount);
         stage_end(st);
         stage_begin(3, st);
-        hipLaunchKernelGGL(k_select, dim3(nlevels, B), dim3(64), 0, st, d_cand, d_cellCount, g, d_cells, d_lvl,
-                           d_lvlCount);
+        hipLaunchKernelGGL(k_select, dim3(nlevels, B), dim3(256), selectLds, st, d_pyr, d_cand, d_cand2, d_cellCount, g,
+                           d_cells, d_lvl, d_lvlCount);
         stage_end(st);
         stage_begin(4, st);
-        hipLaunchKernelGGL(k_blur, dim3(nTiles, B), dim3(256), 0, st, d_pyr, d_blur, g, d_tiles);
-        stage_end(st);
-        stage_begin(5, st);
         dim3 gd((std::max(kpCap, 1) + 3) / 4, B);
         hipLaunchKernelGGL(k_orient_desc, gd, dim3(256), 0, st, d_pyr, d_blur, g, d_lvl, d_lvlCount, kps, desc,
                            counts);
@@ -1724,7 +1958,7 @@ int orb_search_for_initialization(const orb_keypoint_t* kps1, const uint8_t* des
     return ORB_OK;
 }
 
-static const char* kStageNames[] = {"k_pyr0", "k_pyr_resize", "k_fast_cells", "k_select", "k_blur", "k_orient_desc"};
+static const char* kStageNames[] = {"k_pyr0", "k_pyr_resize", "k_level", "k_select", "k_orient_desc"};
 
 int orb_profile_enable(orb_extractor_t* h, int enable) {
     if (!h) return set_err(ORB_EINVAL, "bad handle");

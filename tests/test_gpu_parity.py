@@ -86,6 +86,17 @@ def test_extract_parity_odd_sizes(W, H):
         _check_frame(ext, ora, img)
 
 
+@pytest.mark.parametrize("W,H,nf,nl,th", [(161, 121, 2000, 4, 20), (160, 120, 2000, 4, 7), (128, 96, 1500, 5, 12),
+                                           (200, 150, 2000, 3, 20), (176, 144, 2000, 3, 7)])
+def test_extract_parity_dense_cell_grids(W, H, nf, nl, th):
+    """Many small cells: the ceil'd cell size makes the non-last cells' detection areas reach
+    past maxBorder (ORBextractor.cc:572-597), so FAST runs beyond h-16 / w-16 there."""
+    ext = orb.ORBextractor(nf, 1.2, nl, orb.FAST_SCORE, th, device=0)
+    ora = Oracle(nf, 1.2, nl, 1, th)
+    for img in orb.synth_stream(W, H, stream=17, first=0, count=2):
+        _check_frame(ext, ora, img)
+
+
 @pytest.mark.parametrize("kind", [orb.SYN_FLAT, orb.SYN_LOWTEX, orb.SYN_NOISE])
 def test_extract_parity_edge_frames(kind):
     ext = orb.ORBextractor(1000, 1.2, 8, orb.FAST_SCORE, 20, device=0)
