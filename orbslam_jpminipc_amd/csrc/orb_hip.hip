@@ -620,64 +620,78 @@ struct BlurTile {
 
 __device__ __forceinline__ int byte_of(uint32_t w, int k) { return (int)((w >> (8 * k)) & 0xFFu); }
 
-#define LVL_FQ 512  // per-wave FAST queue capacity (u16 entries)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef short i16x2 __attribute__((ext_vector_type(2)));
 
-// Full 9-arc test + exact strength on a wave's pre-filter queue (pq, qn entries of
-// (row << 8 | col) in the wave's rows of the staged tile); corners are appended to the
-// (frame, level) list as (S << 24) | (y << 12) | x.  Rare enough to live out of line.
+// Gaussian taps (18, 34, 49, 55, 49, 34, 18) = getGaussianKernel(7, 2) in 8-bit fixed point
+// (the host checks its own restatement against these).  Horizontal pass: two
+// v_dot4_u32_u8 per pixel on byte windows [x-3, x] and [x+1, x+4].
+#define GT_WA 0x37312212u  // bytes (x-3, x-2, x-1, x) -> 18, 34, 49, 55
+#define GT_WB 0x00122231u  // bytes (x+1, x+2, x+3, x+4) -> 49, 34, 18, 0
+// Vertical pass in packed fp32 with the 2^-16 output scale folded into the taps: every
+// partial sum is an integer < 2^24 times 2^-16, so the FMAs are exact (only a saturating
+// T >= 2^24 can round, and it clamps to 255 either way).
+#define GV0 (55.0f / 65536.0f)
+#define GV1 (49.0f / 65536.0f)
+#define GV2 (34.0f / 65536.0f)
+#define GV3 (18.0f / 65536.0f)
+
+// Per-wave FAST queue: every lane-row of the wave's rows (and its share of the halo ring)
+// fits, so the queue is drained once, after the row loop.  u16 entry = rowCode << 11 |
+// laneCode << 4 | mask: tile row = wave*BLUR_RW - 1 + rowCode (0..17), bit j of mask is tile
+// column 4*(laneCode-1) + j (laneCode 0 and 65 carry the halo columns -1 and 256).
+#define LVL_FQ (18 * 64 + 2 * 18)
+#define LVL_CQ 256   // per-wave corner / survivor chunk (u16 entries)
 #define LVL_SPW 264  // LDS strength-plane row pitch (bytes): tile columns -4 .. 259
 
-// Full 9-arc test + exact strength on a wave's FAST queue (pq, qn entries of
-// ((row + 1) << 9) | (col + 1), tile-relative, row in [-1, TH], col in [-1, 256]); corners
-// store S into the tile's strength plane Sp (row + 1, col + 4).  Out of line: runs once per
-// ~256 queued pixels of a wave.
-__device__ __attribute__((noinline)) void level_drain(const uint8_t* inb, uint16_t* pq, uint16_t* cq, int qn, int ft,
-                                                      uint8_t* Sp, int lane) {
-    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    const int TP = BLUR_IW * 4;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    int cn = 0;
-    for (int i0 = 0; i0 < qn; i0 += 64) {
-        const int i = i0 + lane;
-        bool corner = false;
-        uint16_t e = 0;
-        if (i < qn) {
-            e = pq[i];
-            const uint8_t* p = inb + ((e >> 9) + 3) * TP + (e & 511) + 3;
-            corner = fast_is_corner(p, TP, ft);
-        }
-        const uint64_t m = __ballot(corner);
-        if (corner) cq[cn + __popcll(m & below)] = e;
-        cn += __popcll(m);
+// Compass pre-filter of cv::FAST (a 9-arc always covers two cyclically adjacent points of
+// {0, 4, 8, 12}) for the 4 pixels of a dword, in packed 16-bit arithmetic: even and odd
+// bytes are split into u16 pairs; q > v + t <=> (v + t) - q < 0 and q < v - t <=> q - (v - t)
+// < 0 (all values within i16).  Returns a 4-bit mask (bit j = pixel j passes).
+__device__ __forceinline__ uint32_t compass4(uint32_t c, uint32_t q0, uint32_t q4, uint32_t q8, uint32_t q12,
+                                             uint32_t tt) {
+    uint32_t pass[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const uint32_t sel = h ? 0x0c030c01u : 0x0c020c00u;  // odd / even bytes -> u16 lanes
+        const i16x2 v = __builtin_bit_cast(i16x2, __builtin_amdgcn_perm(0u, c, sel));
+        const i16x2 a = __builtin_bit_cast(i16x2, __builtin_amdgcn_perm(0u, q0, sel));
+        const i16x2 b = __builtin_bit_cast(i16x2, __builtin_amdgcn_perm(0u, q4, sel));
+        const i16x2 d = __builtin_bit_cast(i16x2, __builtin_amdgcn_perm(0u, q8, sel));
+        const i16x2 e = __builtin_bit_cast(i16x2, __builtin_amdgcn_perm(0u, q12, sel));
+        const i16x2 t = __builtin_bit_cast(i16x2, tt);
+        const i16x2 hi = v + t, lo = v - t;
+        const uint32_t b0 = __builtin_bit_cast(uint32_t, (i16x2)(hi - a)), b4 = __builtin_bit_cast(uint32_t, (i16x2)(hi - b));
+        const uint32_t b8 = __builtin_bit_cast(uint32_t, (i16x2)(hi - d)), b12 = __builtin_bit_cast(uint32_t, (i16x2)(hi - e));
+        const uint32_t d0 = __builtin_bit_cast(uint32_t, (i16x2)(a - lo)), d4 = __builtin_bit_cast(uint32_t, (i16x2)(b - lo));
+        const uint32_t d8 = __builtin_bit_cast(uint32_t, (i16x2)(d - lo)), d12 = __builtin_bit_cast(uint32_t, (i16x2)(e - lo));
+        // some cyclically adjacent pair of {0,4,8,12}: (m0 | m8) & (m4 | m12)
+        pass[h] = (((b0 | b8) & (b4 | b12)) | ((d0 | d8) & (d4 | d12))) & 0x80008000u;
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    for (int i = lane; i < cn; i += 64) {
-        const uint16_t e = cq[i];
-        const uint8_t* p = inb + ((e >> 9) + 3) * TP + (e & 511) + 3;
-        Sp[(e >> 9) * LVL_SPW + (e & 511) + 3] = (uint8_t)fast_exact_strength(p, TP);
-    }
+    // bit 15 / 31 of even -> pixels 0 / 2, of odd -> pixels 1 / 3
+    return ((pass[0] >> 15) & 1u) | ((pass[1] >> 14) & 2u) | ((pass[0] >> 29) & 4u) | ((pass[1] >> 28) & 8u);
 }
 
 // One tile of one level, four waves of BLUR_RW rows:
-//   (1) the descriptor image rows of the wave (blur);
-//   (2) FAST at fastTh inside the detection region [16, w-16) x [16, h-16): compass pre-filter
-//       on 4 px per lane from the dword rings the blur already holds, survivors queued per
-//       wave; the full 9-arc test and the exact strength S run on the queue with all lanes
-//       busy (level_drain) and land in an LDS strength plane, which also holds the tile's 1-px
-//       halo ring (queued without pre-filter);
+//   (1) the descriptor image rows of the wave (blur: dot4 rows, packed-fp32 columns);
+//   (2) FAST at fastTh inside the detection region [16, detX1) x [16, detY1): compass
+//       pre-filter on the lane's 4 pixels (packed 16-bit), lane-rows with a survivor queued
+//       per wave; the full 9-arc test and the exact strength S run on the queue with all
+//       lanes busy after the row loop, and land in an LDS strength plane, which also holds the
+//       tile's 1-px halo ring (queued without pre-filter);
 //   (3) after one barrier, the per-cell 3x3 NMS of cv::FAST(cellImage, fastTh, true)
 //       (ORBextractor.cc:599-607) from the plane: a corner survives iff S-1 beats the score of
 //       each 8-neighbour inside its cell's detection area (S-1 for a corner, else 0).
 //       Survivors are appended to their cell's candidate slots as ((S-1) << 24) | (y << 12) | x;
 //       cells tile the detection region, so (cell row, col) = ((y-16)/cellH, (x-16)/cellW).
 //       k_select restores raster order.
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
-k_level(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur, Geom g, const BlurTile* __restrict__ tiles,
-        const CellGeom* __restrict__ cells, uint32_t* __restrict__ cand, int* __restrict__ cellCount) {
+__global__ void __launch_bounds__(256) k_level(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur, Geom g,
+                                               const BlurTile* __restrict__ tiles, const CellGeom* __restrict__ cells,
+                                               uint32_t* __restrict__ cand, int* __restrict__ cellCount) {
     __shared__ __attribute__((aligned(16))) uint32_t s_in[(BLUR_TH + 8) * BLUR_IW];
     __shared__ __attribute__((aligned(16))) uint8_t s_S[(BLUR_TH + 2) * LVL_SPW];
     __shared__ uint16_t s_pq[4][LVL_FQ];
-    __shared__ uint16_t s_cq[4][LVL_FQ];
+    __shared__ uint16_t s_cq[4][LVL_CQ];
     const BlurTile t = tiles[blockIdx.x];
     const int b = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const LevelGeom& lg = g.lv[t.level];
@@ -695,42 +709,42 @@ k_level(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur, Geom g, con
     __syncthreads();
     const uint8_t* inb = (const uint8_t*)s_in;
     const int ft = g.fastTh;
+    const uint32_t tt = (uint32_t)ft | ((uint32_t)ft << 16);
     const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint16_t* pq = s_pq[wave];
     uint16_t* cq = s_cq[wave];
+    const int x = t.x0 + 4 * lane;  // first of this lane's 4 columns
+    const int rBase = wave * BLUR_RW - 1;  // tile row of rowCode 0
+    // detection-region columns of this lane (4-bit mask, lane constant)
+    uint32_t colMask = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) colMask |= (uint32_t)(x + j >= EDGE && x + j < lg.detX1) << j;
     int qn = 0;
-    {  // halo ring of the strength plane: row -1 (wave 0), row TH (wave 3), columns -1 and 256
-        auto inDet = [&](int rt, int ct) {
-            const int X = t.x0 + ct, Y = t.y0 + rt;
-            return X >= EDGE && X < lg.detX1 && Y >= EDGE && Y < lg.detY1;
-        };
-        auto push = [&](bool v, int rt, int ct) {
-            const uint64_t m = __ballot(v);
-            if (v) pq[qn + __popcll(m & below)] = (uint16_t)(((rt + 1) << 9) | (ct + 1));
-            qn += __popcll(m);
-        };
+    auto push = [&](uint32_t mask, int rt, int laneCode) {  // wave-uniform call
+        const bool v = mask != 0u;
+        const uint64_t m = __ballot(v);
+        if (v) pq[qn + __popcll(m & below)] = (uint16_t)(((rt - rBase) << 11) | (laneCode << 4) | mask);
+        qn += __popcll(m);
+    };
+    {  // halo ring of the strength plane: rows -1 (wave 0) and TH (wave 3) over the tile's
+       // columns, columns -1 and 256 over rows -1 .. TH (no pre-filter)
         if (wave == 0 || wave == 3) {
             const int rt = wave == 0 ? -1 : BLUR_TH;
-            for (int c0 = -1; c0 <= BLUR_TW; c0 += 64) {
-                const int ct = c0 + lane;
-                push(ct <= BLUR_TW && inDet(rt, ct), rt, ct);
-            }
+            const int Y = t.y0 + rt;
+            push((Y >= EDGE && Y < lg.detY1) ? colMask : 0u, rt, lane + 1);
         }
-        {
-            const int rt = wave * BLUR_RW + (lane & 15), ct = (lane & 16) ? BLUR_TW : -1;
-            push(lane < 32 && inDet(rt, ct), rt, ct);
-        }
-        if (qn > LVL_FQ - 256) {
-            level_drain(inb, pq, cq, qn, ft, s_S, lane);
-            qn = 0;
-        }
+        const int nr = BLUR_RW + (wave == 0) + (wave == 3);  // rows of this wave's column halo
+        const int r0 = wave * BLUR_RW - (wave == 0);
+        const int rt = r0 + (lane >> 1), right = lane & 1;
+        const int X = t.x0 + (right ? BLUR_TW : -1), Y = t.y0 + rt;
+        const bool in = lane < 2 * nr && X >= EDGE && X < lg.detX1 && Y >= EDGE && Y < lg.detY1;
+        push(in ? (right ? 1u : 8u) : 0u, rt, right ? 65 : 0);
     }
-    const int x = t.x0 + 4 * lane;  // first of this lane's 4 output columns
     const bool colLive = x < lg.w + 4;
-    const int k0 = g.taps[0], k1 = g.taps[1], k2 = g.taps[2], k3 = g.taps[3];
+    const bool lanePlain = x >= 0 && x + 3 < lg.xsimd_blur;  // all 4 px inside the ROI, SSE2 columns
     const uint32_t* in = s_in + (wave * BLUR_RW + 1) * BLUR_IW + lane;
-    int R[7][4];
-    uint32_t C[7], A[7], Z[7];  // dwords of each ring row: centre (x..x+3), left (x-4..x-1), right (x+4..x+7)
+    f32x2 R[7][2];  // horizontal sums of the ring rows, pixels (0,1) and (2,3)
+    uint32_t C[7];  // centre dwords (x .. x+3) of the ring rows
     bool done = false;
     for (int r0 = 0; r0 < BLUR_RW + 6 && !done; r0 += 7) {
 #pragma unroll
@@ -738,19 +752,21 @@ k_level(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur, Geom g, con
             const int r = r0 + k;
             if (done || r >= BLUR_RW + 6) break;
             const uint32_t d0 = in[r * BLUR_IW], d1 = in[r * BLUR_IW + 1], d2 = in[r * BLUR_IW + 2];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int b1 = byte_of(j < 3 ? d0 : d1, (j + 1) & 3), b2 = byte_of(j < 2 ? d0 : d1, (j + 2) & 3);
-                const int b3 = byte_of(j < 1 ? d0 : d1, (j + 3) & 3), b4 = byte_of(d1, j);
-                const int b5 = byte_of(j < 3 ? d1 : d2, (j + 1) & 3), b6 = byte_of(j < 2 ? d1 : d2, (j + 2) & 3);
-                const int b7 = byte_of(j < 1 ? d1 : d2, (j + 3) & 3);
-                R[k][j] = k0 * b4 + k1 * (b3 + b5) + k2 * (b2 + b6) + k3 * (b1 + b7);
+            {
+                const uint32_t h0 = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 1), GT_WA,
+                                                           __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 1), GT_WB, 0u, false), false);
+                const uint32_t h1 = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 2), GT_WA,
+                                                           __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 2), GT_WB, 0u, false), false);
+                const uint32_t h2 = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 3), GT_WA,
+                                                           __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 3), GT_WB, 0u, false), false);
+                const uint32_t h3 = __builtin_amdgcn_udot4(d1, GT_WA, __builtin_amdgcn_udot4(d2, GT_WB, 0u, false), false);
+                R[k][0] = (f32x2){(float)h0, (float)h1};
+                R[k][1] = (f32x2){(float)h2, (float)h3};
             }
             C[k] = d1;
-            A[k] = d0;
-            Z[k] = d2;
             if (r < 6) continue;
-            const int y = t.y0 + wave * BLUR_RW + (r - 6);  // output row; ring slot (k+4)%7 is its centre
+            const int rt = wave * BLUR_RW + (r - 6);  // output row (tile); ring slot (k+4)%7 is its centre
+            const int y = t.y0 + rt;
             if (y >= lg.h + 3) {
                 done = true;
                 break;
@@ -758,115 +774,155 @@ k_level(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur, Geom g, con
             const int kc = (k + 4) % 7, km1 = (k + 3) % 7, kp1 = (k + 5) % 7, km2 = (k + 2) % 7, kp2 = (k + 6) % 7,
                       km3 = (k + 1) % 7;
             if (colLive) {
-                const bool rowIn = y >= 0 && y < lg.h;
-                const uint32_t craw = C[kc];
-                uint32_t word = 0;
+                uint32_t word;
+                if (y >= 0 && y < lg.h) {
+                    f32x2 v[2];
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int xj = x + j;
-                    int v;
-                    if (rowIn && xj >= 0 && xj < lg.w) {
-                        const int T = k0 * R[kc][j] + k1 * (R[km1][j] + R[kp1][j]) + k2 * (R[km2][j] + R[kp2][j]) +
-                                      k3 * (R[km3][j] + R[k][j]);
-                        v = xj < lg.xsimd_blur ? (T + 32767 + ((T >> 16) & 1)) >> 16 : (T + 32768) >> 16;
-                        v = min(v, 255);
-                    } else {
-                        v = byte_of(craw, j);  // outside the ROI: the un-blurred padding
+                    for (int h = 0; h < 2; ++h) {
+                        f32x2 acc = R[kc][h] * (f32x2){GV0, GV0};
+                        acc = __builtin_elementwise_fma(R[km1][h] + R[kp1][h], (f32x2){GV1, GV1}, acc);
+                        acc = __builtin_elementwise_fma(R[km2][h] + R[kp2][h], (f32x2){GV2, GV2}, acc);
+                        acc = __builtin_elementwise_fma(R[km3][h] + R[k][h], (f32x2){GV3, GV3}, acc);
+                        v[h] = acc;
                     }
-                    word |= (uint32_t)v << (8 * j);
+                    const float vv[4] = {v[0].x, v[0].y, v[1].x, v[1].y};
+                    if (lanePlain) {
+                        word = 0u;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            word = __builtin_amdgcn_cvt_pk_u8_f32(fminf(__builtin_rintf(vv[j]), 255.0f), j, word);
+                    } else {  // ROI edge lanes: raw padding outside, half-up rounding on the tail
+                        const uint32_t craw = C[kc];
+                        word = 0u;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const int xj = x + j;
+                            uint32_t bj;
+                            if (xj < 0 || xj >= lg.w) {
+                                bj = (uint32_t)byte_of(craw, j);
+                            } else {
+                                const float rr = xj < lg.xsimd_blur ? __builtin_rintf(vv[j]) : floorf(vv[j] + 0.5f);
+                                bj = (uint32_t)fminf(rr, 255.0f);
+                            }
+                            word |= bj << (8 * j);
+                        }
+                    }
+                } else {
+                    word = C[kc];  // outside the ROI rows: the un-blurred padding
                 }
                 *(uint32_t*)(dst + (long long)(y + EDGE) * lg.pitch + (x + EDGE)) = word;
             }
             // FAST pre-filter for the row (wave-uniform row test)
             if (y >= EDGE && y < lg.detY1) {
-                const uint32_t cc = C[kc], cd = C[k], cu = C[km3];
-                const uint32_t a4 = __builtin_amdgcn_alignbyte(Z[kc], cc, 3);   // x+3 .. x+6
-                const uint32_t a12 = __builtin_amdgcn_alignbyte(cc, A[kc], 1);  // x-3 .. x
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int xj = x + j;
-                    const int v = byte_of(cc, j), hi = v + ft, lo = v - ft;
-                    const int q0 = byte_of(cd, j), q4 = byte_of(a4, j), q8 = byte_of(cu, j), q12 = byte_of(a12, j);
-                    const int bm = (q0 > hi) | ((q4 > hi) << 1) | ((q8 > hi) << 2) | ((q12 > hi) << 3);
-                    const int dm = (q0 < lo) | ((q4 < lo) << 1) | ((q8 < lo) << 2) | ((q12 < lo) << 3);
-                    const bool pre = xj >= EDGE && xj < lg.detX1 &&
-                                     (((bm & ((bm >> 1) | (bm << 3))) | (dm & ((dm >> 1) | (dm << 3)))) & 0xF);
-                    const uint64_t m = __ballot(pre);
-                    if (pre) pq[qn + __popcll(m & below)] = (uint16_t)(((wave * BLUR_RW + r - 5) << 9) | (4 * lane + j + 1));
-                    qn += __popcll(m);
-                }
-                if (qn > LVL_FQ - 256) {
-                    level_drain(inb, pq, cq, qn, ft, s_S, lane);
-                    qn = 0;
-                }
+                const uint32_t cc = C[kc];
+                const uint32_t* ic = in + (r - 3) * BLUR_IW;  // centre row in LDS
+                const uint32_t a4 = __builtin_amdgcn_alignbyte(ic[2], cc, 3);   // x+3 .. x+6
+                const uint32_t a12 = __builtin_amdgcn_alignbyte(cc, ic[0], 1);  // x-3 .. x
+                const uint32_t mask = compass4(cc, C[k], a4, C[km3], a12, tt) & colMask;
+                push(mask, rt, lane + 1);
             }
         }
     }
-    if (qn) level_drain(inb, pq, cq, qn, ft, s_S, lane);
+    // full 9-arc test + exact strength on the queue, all lanes busy; corners -> plane
+    {
+        const int TP = BLUR_IW * 4;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        for (int i0 = 0; i0 < qn; i0 += 64) {
+            const int i = i0 + lane;
+            const uint32_t e = i < qn ? pq[i] : 0u;
+            const int rt = rBase + (int)(e >> 11), cb = 4 * ((int)((e >> 4) & 127) - 1);
+            int cn = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                bool corner = false;
+                if ((e >> j) & 1u) corner = fast_is_corner(inb + (rt + 4) * TP + cb + j + 4, TP, ft);
+                const uint64_t m = __ballot(corner);
+                if (corner) cq[cn + __popcll(m & below)] = (uint16_t)(((rt + 1) << 9) | (cb + j + 1));
+                cn += __popcll(m);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            for (int k = lane; k < cn; k += 64) {
+                const uint16_t c = cq[k];
+                const uint8_t* p = inb + ((c >> 9) + 3) * TP + (c & 511) + 3;
+                s_S[(c >> 9) * LVL_SPW + (c & 511) + 3] = (uint8_t)fast_exact_strength(p, TP);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+    }
     __syncthreads();
-    // (3) in-cell NMS over the wave's rows of the plane, 4 columns per lane.  Cell (i, j) has
-    // the detection area [16 + j*cellW, j == cols-1 ? w-16 : 16 + (j+1)*cellW) in x (likewise
-    // in y), ORBextractor.cc:572-597.
-    auto cellRange = [](int v, int n, int cs, int lim, int& k, int& lo, int& hi) {
-        k = (v - EDGE) / cs;
-        lo = EDGE + k * cs;
-        hi = k == n - 1 ? lim - EDGE : lo + cs;
-    };
+    // (3) in-cell NMS.  Cell (i, j) has the detection area [16 + j*cellW, j == cols-1 ? w-16 :
+    // 16 + (j+1)*cellW) in x (likewise in y), ORBextractor.cc:572-597.
     const CellGeom* lc = cells + lg.cell0;
     int* fcount = cellCount + (long long)b * g.nCells + lg.cell0;
     uint32_t* fcand = cand + (long long)b * g.candPerFrame;
-    auto emit = [&](int n) {  // all lanes in parallel
+    // corners of the wave's rows (ballot-compacted from the plane), then the NMS on the list
+    int cn = 0;
+    auto nms_emit = [&](int n) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        for (int k = lane; k < n; k += 64) {
-            const uint16_t e = cq[k];
-            const int rte = e >> 9, ct = e & 511;
-            const int X = t.x0 + ct, Ye = t.y0 + rte;
-            const int c = ((Ye - EDGE) / lg.cellH) * lg.cols + (X - EDGE) / lg.cellW;
-            const int S = s_S[(rte + 1) * LVL_SPW + ct + 4];
+        int sn = 0;
+        for (int k0 = 0; k0 < n; k0 += 64) {
+            const int k = k0 + lane;
+            bool keep = false;
+            uint16_t e = 0;
+            if (k < n) {
+                e = pq[k];
+                const int rt = e >> 9, ct = e & 511;
+                const int X = t.x0 + ct, Y = t.y0 + rt;
+                const int ci = (Y - EDGE) / lg.cellH, cj = (X - EDGE) / lg.cellW;
+                if (ci < lg.rows && cj < lg.cols) {
+                    const int xlo = EDGE + cj * lg.cellW, xhi = cj == lg.cols - 1 ? lg.w - EDGE : xlo + lg.cellW;
+                    const int ylo = EDGE + ci * lg.cellH, yhi = ci == lg.rows - 1 ? lg.h - EDGE : ylo + lg.cellH;
+                    const uint8_t* sp = s_S + (rt + 1) * LVL_SPW + ct + 4;
+                    const int S = sp[0];
+                    keep = true;
+#pragma unroll
+                    for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+                        for (int dx = -1; dx <= 1; ++dx) {
+                            if (dx == 0 && dy == 0) continue;
+                            const bool inCell = X + dx >= xlo && X + dx < xhi && Y + dy >= ylo && Y + dy < yhi;
+                            const int nb = inCell ? sp[dy * LVL_SPW + dx] : 0;
+                            keep = keep && (S - 1 > (nb ? nb - 1 : 0));
+                        }
+                }
+            }
+            // survivors overwrite the front of the chunk (k0 + 64 > sn: no unread entry is hit)
+            const uint64_t m = __ballot(keep);
+            if (keep) pq[sn + __popcll(m & below)] = e;
+            sn += __popcll(m);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        for (int k = lane; k < sn; k += 64) {
+            const uint16_t e = pq[k];
+            const int rt = e >> 9, ct = e & 511;
+            const int X = t.x0 + ct, Y = t.y0 + rt;
+            const int c = ((Y - EDGE) / lg.cellH) * lg.cols + (X - EDGE) / lg.cellW;
+            const int S = s_S[(rt + 1) * LVL_SPW + ct + 4];
             const int cap = lc[c].cap, off = lc[c].candOff;
             const int pos = atomicAdd(fcount + c, 1);
-            if (pos < cap) fcand[off + pos] = ((uint32_t)(S - 1) << 24) | ((uint32_t)Ye << 12) | (uint32_t)X;
+            if (pos < cap) fcand[off + pos] = ((uint32_t)(S - 1) << 24) | ((uint32_t)Y << 12) | (uint32_t)X;
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     };
-    int cjs[4], xlo[4], xhi[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) cellRange(max(t.x0 + 4 * lane + j, EDGE), lg.cols, lg.cellW, lg.w, cjs[j], xlo[j], xhi[j]);
-    int cn = 0;
     for (int i = 0; i < BLUR_RW; ++i) {
         const int rt = wave * BLUR_RW + i;
         const int Y = t.y0 + rt;
         if (Y < EDGE || Y >= lg.detY1) continue;  // wave-uniform
-        int ci, ylo, yhi;
-        cellRange(Y, lg.rows, lg.cellH, lg.h, ci, ylo, yhi);
         const uint32_t w4 = *(const uint32_t*)(s_S + (rt + 1) * LVL_SPW + 4 + 4 * lane);
+        if (__ballot(w4 != 0u) == 0ull) continue;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const int S = (w4 >> (8 * j)) & 0xFF;
-            bool keep = S != 0 && ci < lg.rows && cjs[j] < lg.cols;
-            if (keep) {
-                const int ct = 4 * lane + j, X = t.x0 + ct;
-                const uint8_t* sp = s_S + (rt + 1) * LVL_SPW + ct + 4;
-#pragma unroll
-                for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-                    for (int dx = -1; dx <= 1; ++dx) {
-                        if (dx == 0 && dy == 0) continue;
-                        const bool inCell = X + dx >= xlo[j] && X + dx < xhi[j] && Y + dy >= ylo && Y + dy < yhi;
-                        const int n = inCell ? sp[dy * LVL_SPW + dx] : 0;
-                        keep = keep && (S - 1 > (n ? n - 1 : 0));
-                    }
-            }
-            const uint64_t m = __ballot(keep);
-            if (keep) cq[cn + __popcll(m & below)] = (uint16_t)((rt << 9) | (4 * lane + j));
+            const bool v = ((w4 >> (8 * j)) & 0xFFu) != 0u;
+            const uint64_t m = __ballot(v);
+            if (v) pq[cn + __popcll(m & below)] = (uint16_t)((rt << 9) | (4 * lane + j));
             cn += __popcll(m);
         }
         if (cn > LVL_FQ - 256) {
-            emit(cn);
+            nms_emit(cn);
             cn = 0;
         }
     }
-    if (cn) emit(cn);
+    if (cn) nms_emit(cn);
 }
 
 // ---- orientation + descriptor -------------------------------------------------------------
@@ -1427,6 +1483,8 @@ struct orb_extractor {
         int k7[7];
         gaussian_taps7(k7);
         for (int i = 0; i < 4; ++i) G.taps[i] = k7[3 + i];
+        if (G.taps[0] != 55 || G.taps[1] != 49 || G.taps[2] != 34 || G.taps[3] != 18)
+            return set_err(ORB_EINVAL, "Gaussian taps differ from the kernel's constants (GT_WA/GT_WB)");
         for (int v = 0; v < 16; ++v) G.umax[v] = umax[v];
         std::vector<CellGeom> cl;
         std::vector<int> rt;
