@@ -130,6 +130,151 @@ int orb_search_for_initialization_batch_device(const orb_keypoint_t* d_kps, cons
                                                int check_ori, int window, float* d_prev_xy, int32_t* d_matches12,
                                                int32_t* d_nmatches, void* stream);
 
+/* ---- the rest of the ORBmatcher family (GPU: csrc/orb_match.hip) ------------------- */
+/* All entry points below take HOST buffers, run on the device of `device`, and are
+ * synchronous.  Map state the reference reads through MapPoint / KeyFrame methods
+ * (isBad, IsInKeyFrame, "already found" sets, outlier flags) arrives as caller-evaluated
+ * per-element `usable` / `taken` flags; each entry point names the reference condition its
+ * flags encode.  Results are indices (the caller maps them back to MapPoint*), so no map
+ * object crosses the boundary.  Pose-level cv::Mat algebra the reference performs once per
+ * call (Scw decomposition, Sim3 composition, -R^T t) is done by the caller with the
+ * reference's own expressions and passed in; the per-point geometry runs on the device. */
+
+#define ORB_MAX_VIEW_LEVELS 16
+
+/* A Frame or KeyFrame as the matchers see it (reference Frame.h:43-138, KeyFrame.h). */
+typedef struct orb_frame_view {
+    const orb_keypoint_t* kps;  /* mvKeysUn, n records                                   */
+    const uint8_t* desc;        /* mDescriptors, n x 32 bytes row-major                  */
+    int32_t n;
+    int32_t nlevels;            /* mnScaleLevels (<= ORB_MAX_VIEW_LEVELS)                */
+    orb_frame_bounds_t bounds;  /* mnMinX .. mnMaxY; grid = 64 x 48 cells over them       */
+    float scale_factors[ORB_MAX_VIEW_LEVELS]; /* mvScaleFactors (Frame.cc:95-103)        */
+    float level_sigma2[ORB_MAX_VIEW_LEVELS];  /* mvLevelSigma2                           */
+    float fx, fy, cx, cy;       /* calibration                                            */
+    float Rcw[9];               /* rotation world->camera, row-major (mRcw / GetRotation) */
+    float tcw[3];               /* translation (mtcw / GetTranslation)                    */
+    float Ow[3];                /* camera centre (mOw / GetCameraCenter)                  */
+} orb_frame_view_t;
+
+/* MapPoint attributes read by the projection matchers (reference MapPoint.h). */
+typedef struct orb_map_points {
+    const float* pos;     /* n x 3 GetWorldPos                                            */
+    const float* normal;  /* n x 3 GetNormal (NULL where unused)                          */
+    const float* dmin;    /* n GetMinDistanceInvariance (NULL where unused)               */
+    const float* dmax;    /* n GetMaxDistanceInvariance (NULL where unused)               */
+    const uint8_t* desc;  /* n x 32 GetDescriptor (NULL where the frame's row is used)    */
+    int32_t n;
+} orb_map_points_t;
+
+/* DBoW2::FeatureVector (std::map<NodeId, vector<unsigned>>, FeatureVector.h:21-49) as CSR:
+ * ascending node ids nodes[n_nodes], offsets[n_nodes + 1], feature indices features[]. */
+typedef struct orb_feature_vector {
+    const uint32_t* nodes;
+    const int32_t* offsets;
+    const int32_t* features;
+    int32_t n_nodes;
+} orb_feature_vector_t;
+
+/* Frame::GetFeaturesInArea (Frame.cc:200-265) for q query windows (min/max level -1 = any),
+ * or KeyFrame::GetFeaturesInArea (KeyFrame.cc:612-652, no level filter, `<= r`) when
+ * keyframe != 0.  Output CSR: out_offsets[q + 1], out_indices[capacity]; ORB_ERANGE if the
+ * candidates exceed `capacity` (out_offsets[q] then holds the required size). */
+int orb_features_in_area(const orb_frame_view_t* view, int keyframe, int q, const float* x, const float* y,
+                         const float* r, const int32_t* min_level, const int32_t* max_level, int32_t* out_offsets,
+                         int32_t* out_indices, int capacity, int device);
+
+/* Frame::isInFrustum (Frame.cc:137-198) for every MapPoint: in_view[i] (mbTrackInView),
+ * proj_x/proj_y (mTrackProjX/Y), level (mnTrackScaleLevel), view_cos (mTrackViewCos).
+ * mps.normal/dmin/dmax required. */
+int orb_frame_is_in_frustum(const orb_frame_view_t* F, orb_map_points_t mps, float viewing_cos_limit,
+                            uint8_t* in_view, float* proj_x, float* proj_y, int32_t* level, float* view_cos,
+                            int device);
+
+/* SearchByBoW(KeyFrame*, Frame&, vpMapPointMatches) (ORBmatcher.cc:155-284).
+ * kf_usable[i]: vpMapPointsKF[i] && !isBad().  f_match[j] = KF keypoint whose MapPoint is
+ * matched to F keypoint j, or -1. */
+int orb_search_by_bow_kf_f(const orb_frame_view_t* KF, const uint8_t* kf_usable, orb_feature_vector_t kf_fv,
+                           const orb_frame_view_t* F, orb_feature_vector_t f_fv, float nnratio, int check_ori,
+                           int32_t* f_match, int* n_matches, int device);
+
+/* SearchByBoW(KeyFrame*, KeyFrame*, vpMatches12) (ORBmatcher.cc:715-850).
+ * usable1/usable2: vpMapPoints[i] && !isBad().  match12[i1] = idx2 or -1. */
+int orb_search_by_bow_kf_kf(const orb_frame_view_t* KF1, const uint8_t* usable1, orb_feature_vector_t fv1,
+                            const orb_frame_view_t* KF2, const uint8_t* usable2, orb_feature_vector_t fv2,
+                            float nnratio, int check_ori, int32_t* match12, int* n_matches, int device);
+
+/* SearchForTriangulation(KF1, KF2, F12, ...) (ORBmatcher.cc:852-1014) with
+ * CheckDistEpipolarLine (136-153).  has_mp1/has_mp2: GetMapPointMatches()[i] != NULL.
+ * F12 row-major 3x3.  match12[i1] = idx2 or -1 (vMatchedPairs = the i1 with match12 >= 0,
+ * ascending). */
+int orb_search_for_triangulation(const orb_frame_view_t* KF1, const uint8_t* has_mp1, orb_feature_vector_t fv1,
+                                 const orb_frame_view_t* KF2, const uint8_t* has_mp2, orb_feature_vector_t fv2,
+                                 const float* F12, float nnratio, int check_ori, int32_t* match12, int* n_matches,
+                                 int device);
+
+/* WindowSearch(F1, F2, windowSize, vpMapPointMatches2, minScaleLevel, maxScaleLevel)
+ * (ORBmatcher.cc:409-516).  usable1[i1]: F1.mvpMapPoints[i1] && !isBad().
+ * match21[i2] = i1 whose MapPoint lands on F2 keypoint i2, or -1. */
+int orb_window_search(const orb_frame_view_t* F1, const uint8_t* usable1, const orb_frame_view_t* F2, int window,
+                      int min_scale_level, int max_scale_level, float nnratio, int check_ori, int32_t* match21,
+                      int* n_matches, int device);
+
+/* SearchByProjection(Frame& F, vector<MapPoint*>, th) (ORBmatcher.cc:49-125) over MapPoints
+ * already projected by Frame::isInFrustum.  usable[i]: mbTrackInView && !isBad();
+ * f_taken[j]: F.mvpMapPoints[j] != NULL on entry.  f_match[j] = MapPoint index newly
+ * assigned to F keypoint j, or -1. */
+int orb_search_by_projection_local(const orb_frame_view_t* F, const uint8_t* f_taken, int n_mp, const uint8_t* usable,
+                                   const float* proj_x, const float* proj_y, const int32_t* level,
+                                   const float* view_cos, const uint8_t* mp_desc, float th, float nnratio,
+                                   int32_t* f_match, int* n_matches, int device);
+
+/* SearchByProjection(Frame& F1, Frame& F2, windowSize, vpMapPointMatches2)
+ * (ORBmatcher.cc:519-594).  mp1.pos: F1's MapPoint positions (row i1); usable1[i1]:
+ * pMP1 && !isBad() && not already in F2.mvpMapPoints; f2_taken[i2]: F2.mvpMapPoints[i2].
+ * match2[i2] = i1 newly assigned, or -1. */
+int orb_search_by_projection_f2f(const orb_frame_view_t* F1, orb_map_points_t mp1, const uint8_t* usable1,
+                                 const orb_frame_view_t* F2, const uint8_t* f2_taken, int window, float nnratio,
+                                 int32_t* match2, int* n_matches, int device);
+
+/* SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, th) (ORBmatcher.cc:
+ * 1507-1620).  usable[i]: LastFrame.mvpMapPoints[i] && !mvbOutlier[i]; mp.pos row i.
+ * cur_match[j] = LastFrame index newly assigned to Current keypoint j, or -1. */
+int orb_search_by_projection_motion(const orb_frame_view_t* Cur, const uint8_t* cur_taken, const orb_frame_view_t* Last,
+                                    orb_map_points_t mp, const uint8_t* usable, float th, int check_ori,
+                                    int32_t* cur_match, int* n_matches, int device);
+
+/* SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, sAlreadyFound, th, ORBdist)
+ * (ORBmatcher.cc:1622-1746).  mp: the KF's MapPoints (pos, dmin, desc) row i; usable[i]:
+ * pMP && !isBad() && !sAlreadyFound.count(pMP).  Cur->Ow = -Rcw^T tcw of the current pose. */
+int orb_search_by_projection_reloc(const orb_frame_view_t* Cur, const uint8_t* cur_taken, const orb_frame_view_t* KF,
+                                   orb_map_points_t mp, const uint8_t* usable, float th, int orb_dist,
+                                   int check_ori, int32_t* cur_match, int* n_matches, int device);
+
+/* SearchByProjection(KeyFrame* pKF, cv::Mat Scw, vpPoints, vpMatched, th) (ORBmatcher.cc:
+ * 286-407).  KF->Rcw/tcw/Ow = the Scw decomposition of 297-302; usable[i]: !isBad() &&
+ * !spAlreadyFound.count(pMP); kf_taken[j]: vpMatched[j].  kf_match[j] = point index or -1. */
+int orb_search_by_projection_sim3(const orb_frame_view_t* KF, const uint8_t* kf_taken, orb_map_points_t pts,
+                                  const uint8_t* usable, int th, int32_t* kf_match, int* n_matches, int device);
+
+/* SearchBySim3(KF1, KF2, vpMatches12, s12, R12, t12, th) (ORBmatcher.cc:1267-1505).
+ * mp1/mp2: the keyframes' MapPoints (pos, dmin, dmax, desc) by keypoint index; usable1/2:
+ * pMP && !vbAlreadyMatched && !isBad().  sR12 = s12*R12, sR21 = (1/s12)*R12^T,
+ * t21 = -sR21*t12 as the reference computes them (1288-1290).  match12[i1] = idx2 for the
+ * mutually agreeing pairs, -1 elsewhere; *n_found = their count. */
+int orb_search_by_sim3(const orb_frame_view_t* KF1, orb_map_points_t mp1, const uint8_t* usable1,
+                       const orb_frame_view_t* KF2, orb_map_points_t mp2, const uint8_t* usable2, const float* sR12,
+                       const float* t12, const float* sR21, const float* t21, float th, int32_t* match12,
+                       int* n_found, int device);
+
+/* Fuse(KeyFrame*, vector<MapPoint*>, th) (ORBmatcher.cc:1016-1134) when scw == 0, or
+ * Fuse(KeyFrame*, cv::Mat Scw, vpPoints, th) (1136-1265) when scw != 0 (KF pose = the Scw
+ * decomposition).  usable[i]: pMP && !isBad() && !IsInKeyFrame (resp. !spAlreadyFound).
+ * best_idx[i] = KF keypoint the point fuses with (bestDist <= TH_LOW), or -1; the caller
+ * applies Replace / AddObservation in point order (the map mutation stays on the host). */
+int orb_fuse(const orb_frame_view_t* KF, orb_map_points_t pts, const uint8_t* usable, float th, int scw,
+             int32_t* best_idx, int* n_fused, int device);
+
 /* ---- measurement ------------------------------------------------------------------- */
 /* Per-stage HIP-event timing of the extraction kernels: when enabled, every
  * orb_extract_batch_device records an event pair around each stage on its launch stream.

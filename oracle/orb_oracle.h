@@ -85,6 +85,41 @@ double oracle_bench(int nfeatures, float scale_factor, int nlevels, int fast_th,
                     int hgt, int stride, int64_t pitch, int threads, int match, int64_t* total_kps,
                     int64_t* total_matches);
 
+/* ---- orb_oracle_match.cpp: the rest of the ORBmatcher family (same arguments as the
+ * corresponding orb_* entry points of include/orb_abi.h, minus `device`) ---------------- */
+int oracle_features_in_area_view(const orb_frame_view_t* view, int keyframe, float x, float y, float r, int min_level,
+                                 int max_level, int32_t* out, int cap);
+int oracle_frame_is_in_frustum(const orb_frame_view_t* F, orb_map_points_t mps, float viewing_cos_limit,
+                               uint8_t* in_view, float* proj_x, float* proj_y, int32_t* level, float* view_cos);
+int oracle_search_by_projection_local(const orb_frame_view_t* F, const uint8_t* f_taken, int n_mp,
+                                      const uint8_t* usable, const float* proj_x, const float* proj_y,
+                                      const int32_t* level, const float* view_cos, const uint8_t* mp_desc, float th,
+                                      float nnratio, int32_t* f_match, int* n_matches);
+int oracle_window_search(const orb_frame_view_t* F1, const uint8_t* usable1, const orb_frame_view_t* F2,
+                         int window, int min_scale_level, int max_scale_level, float nnratio, int check_ori,
+                         int32_t* match21, int* n_matches);
+int oracle_search_by_projection_f2f(const orb_frame_view_t* F1, orb_map_points_t mp1, const uint8_t* usable1,
+                                    const orb_frame_view_t* F2, const uint8_t* f2_taken, int window, float nnratio,
+                                    int32_t* match2, int* n_matches);
+int oracle_search_by_projection_motion(const orb_frame_view_t* Cur, const uint8_t* cur_taken,
+                                       const orb_frame_view_t* Last, orb_map_points_t mp, const uint8_t* usable,
+                                       float th, int check_ori, int32_t* cur_match, int* n_matches);
+int oracle_search_by_projection_reloc(const orb_frame_view_t* Cur, const uint8_t* cur_taken,
+                                      const orb_frame_view_t* KF, orb_map_points_t mp, const uint8_t* usable,
+                                      float th, int orb_dist, int check_ori, int32_t* cur_match, int* n_matches);
+int oracle_search_by_projection_sim3(const orb_frame_view_t* KF, const uint8_t* kf_taken, orb_map_points_t pts,
+                                     const uint8_t* usable, int th, int32_t* kf_match, int* n_matches);
+int oracle_fuse(const orb_frame_view_t* KF, orb_map_points_t pts, const uint8_t* usable, float th, int scw,
+                int32_t* best_idx, int* n_fused);
+int oracle_search_by_sim3(const orb_frame_view_t* KF1, orb_map_points_t mp1, const uint8_t* usable1,
+                          const orb_frame_view_t* KF2, orb_map_points_t mp2, const uint8_t* usable2,
+                          const float* sR12, const float* t12, const float* sR21, const float* t21, float th,
+                          int32_t* match12, int* n_found);
+int oracle_search_for_triangulation(const orb_frame_view_t* KF1, const uint8_t* has_mp1, orb_feature_vector_t fv1,
+                                    const orb_frame_view_t* KF2, const uint8_t* has_mp2, orb_feature_vector_t fv2,
+                                    const float* F12, float nnratio, int check_ori, int32_t* match12,
+                                    int* n_matches);
+
 #ifdef __cplusplus
 }
 #endif

@@ -61,6 +61,45 @@ _i = ctypes.c_int
 _i64 = ctypes.c_int64
 _f = ctypes.c_float
 
+MAX_VIEW_LEVELS = 16
+
+
+class FrameView(ctypes.Structure):
+    """orb_frame_view_t (include/orb_abi.h): a Frame / KeyFrame as the matchers see it."""
+
+    _fields_ = [
+        ("kps", _vp),
+        ("desc", _vp),
+        ("n", ctypes.c_int32),
+        ("nlevels", ctypes.c_int32),
+        ("bounds", FrameBounds),
+        ("scale_factors", _f * MAX_VIEW_LEVELS),
+        ("level_sigma2", _f * MAX_VIEW_LEVELS),
+        ("fx", _f),
+        ("fy", _f),
+        ("cx", _f),
+        ("cy", _f),
+        ("Rcw", _f * 9),
+        ("tcw", _f * 3),
+        ("Ow", _f * 3),
+    ]
+
+
+class MapPoints(ctypes.Structure):
+    """orb_map_points_t: MapPoint attributes read by the projection matchers."""
+
+    _fields_ = [("pos", _vp), ("normal", _vp), ("dmin", _vp), ("dmax", _vp), ("desc", _vp), ("n", ctypes.c_int32)]
+
+
+class FeatureVectorCSR(ctypes.Structure):
+    """orb_feature_vector_t: DBoW2::FeatureVector as CSR (nodes, offsets, features)."""
+
+    _fields_ = [("nodes", _vp), ("offsets", _vp), ("features", _vp), ("n_nodes", ctypes.c_int32)]
+
+
+_pv = ctypes.POINTER(FrameView)
+_pi = ctypes.POINTER(_i)
+
 # name -> (restype, argtypes); every symbol declared in include/orb_abi.h
 HIP_SIGNATURES = {
     "orb_last_error": (ctypes.c_char_p, []),
@@ -83,6 +122,22 @@ HIP_SIGNATURES = {
         _i,
         [_vp, _vp, _vp, _i, _i, _vp, _vp, FrameBounds, _f, _i, _i, _vp, _vp, _vp, _vp],
     ),
+    "orb_features_in_area": (_i, [_pv, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i]),
+    "orb_frame_is_in_frustum": (_i, [_pv, MapPoints, _f, _vp, _vp, _vp, _vp, _vp, _i]),
+    "orb_search_by_bow_kf_f": (_i, [_pv, _vp, FeatureVectorCSR, _pv, FeatureVectorCSR, _f, _i, _vp, _pi, _i]),
+    "orb_search_by_bow_kf_kf": (_i, [_pv, _vp, FeatureVectorCSR, _pv, _vp, FeatureVectorCSR, _f, _i, _vp, _pi, _i]),
+    "orb_search_for_triangulation": (
+        _i,
+        [_pv, _vp, FeatureVectorCSR, _pv, _vp, FeatureVectorCSR, _vp, _f, _i, _vp, _pi, _i],
+    ),
+    "orb_window_search": (_i, [_pv, _vp, _pv, _i, _i, _i, _f, _i, _vp, _pi, _i]),
+    "orb_search_by_projection_local": (_i, [_pv, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp, _f, _f, _vp, _pi, _i]),
+    "orb_search_by_projection_f2f": (_i, [_pv, MapPoints, _vp, _pv, _vp, _i, _f, _vp, _pi, _i]),
+    "orb_search_by_projection_motion": (_i, [_pv, _vp, _pv, MapPoints, _vp, _f, _i, _vp, _pi, _i]),
+    "orb_search_by_projection_reloc": (_i, [_pv, _vp, _pv, MapPoints, _vp, _f, _i, _i, _vp, _pi, _i]),
+    "orb_search_by_projection_sim3": (_i, [_pv, _vp, MapPoints, _vp, _i, _vp, _pi, _i]),
+    "orb_search_by_sim3": (_i, [_pv, MapPoints, _vp, _pv, MapPoints, _vp, _vp, _vp, _vp, _vp, _f, _vp, _pi, _i]),
+    "orb_fuse": (_i, [_pv, MapPoints, _vp, _f, _i, _vp, _pi, _i]),
     "orb_profile_enable": (_i, [_vp, _i]),
     "orb_profile_read": (_i, [_vp, _vp, _vp, _i]),
     "orb_profile_stage_name": (ctypes.c_char_p, [_i]),

@@ -28,6 +28,7 @@
 
 #include "../../include/orb_abi.h"
 #include "nth_select.h"
+#include "orb_internal.h"
 #include "orb_device.h"
 #include "pattern31.inc"
 
@@ -40,10 +41,12 @@
 // ======================================================================================
 static thread_local std::string g_last_error = "";
 
-static int set_err(int code, const std::string& msg) {
+int orb_internal_set_error(int code, const std::string& msg) {
     g_last_error = msg;
     return code;
 }
+
+static int set_err(int code, const std::string& msg) { return orb_internal_set_error(code, msg); }
 
 #define HIP_TRY(expr)                                                                               \
     do {                                                                                            \

@@ -1,0 +1,1636 @@
+// orb_match.hip — MI355X (gfx950) kernels for the ORBmatcher family beyond
+// SearchForInitialization, plus the Frame / KeyFrame window queries they stand on.
+//
+// Every matcher of the reference (ORBmatcher.cc) is the same computation with different
+// knobs: for each query (a MapPoint or a keypoint, in the reference's loop order) build a
+// candidate list on a target frame — a 64 x 48 grid window (Frame::GetFeaturesInArea,
+// KeyFrame::GetFeaturesInArea) or a shared vocabulary node (SearchByBoW) — take the Hamming
+// best (and second best) of the candidates that are not yet taken, accept by a
+// threshold / ratio rule, mark the target taken, and finally drop matches outside the three
+// dominant rotation-histogram bins.  The GPU runs that as four kernels per call:
+//
+//   k_grid_build   one block per target frame: the grid as CSR (cellStart[3073], items[]) in
+//                  cell order ix*48+iy, keypoint index order inside a cell = the reference's
+//                  traversal order (ix outer, iy inner, insertion order).
+//   k_query_prep   one thread per query: the per-query geometry (projection, frustum /
+//                  image / distance / viewing-angle tests, predicted level, window radius).
+//   k_query_scan   one wave per query: every candidate of the window, Hamming distance,
+//                  the 8 smallest (distance, traversal order) keys and the candidate count.
+//                  Targets taken before the call are skipped here (taken only grows).
+//   k_resolve      one block per call: the loop-carried part.  Matchers whose candidate
+//                  loop skips targets taken earlier IN THE SAME CALL (F.mvpMapPoints[idx],
+//                  vpMatched[idx], vbMatched2[idx]) replay the queries in order on one wave:
+//                  best / second = the first untaken entries of the query's top-8; if the
+//                  top-8 runs out the wave rescans the full window against the live taken
+//                  flags (exact).  Then the rotation histogram / ComputeThreeMaxima filter.
+//                  Matchers without that dependency (Fuse, SearchBySim3) resolve in parallel.
+//
+// Arithmetic follows the reference bit for bit: cv::Mat algebra (gemm fast path, norm, dot)
+// in the double/float mix OpenCV 2.4 uses, the reference's own float expressions with the
+// FMA contraction g++ -O3 -march=native applies (explicit __builtin_fmaf; see
+// scripts/contraction_check.sh), IEEE division/sqrt (-fhip-fp32-correctly-rounded-divide-sqrt).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/orb_abi.h"
+#include "orb_device.h"
+#include "orb_internal.h"
+
+using orbdev::hamming256;
+
+namespace {
+
+constexpr int GRID_COLS = 64, GRID_ROWS = 48, NCELLS = GRID_COLS * GRID_ROWS;  // Frame.h:35-36
+constexpr int TOPK = 8;
+constexpr int TH_HIGH = 100, TH_LOW = 50, HISTO = 30;  // ORBmatcher.cc:40-42
+constexpr int MAX_TARGET = 16384;                       // keypoints per target frame (LDS state)
+
+enum Mode : int {
+    M_AREA_F = 0,   // Frame::GetFeaturesInArea
+    M_AREA_KF,      // KeyFrame::GetFeaturesInArea
+    M_LOCAL,        // SearchByProjection(Frame&, vector<MapPoint*>, th)       ORBmatcher.cc:49-125
+    M_WINDOW,       // WindowSearch                                            409-516
+    M_F2F,          // SearchByProjection(Frame&, Frame&, windowSize, ...)     519-594
+    M_MOTION,       // SearchByProjection(Frame&, const Frame&, th)            1507-1620
+    M_RELOC,        // SearchByProjection(Frame&, KeyFrame*, set, th, ORBdist) 1622-1746
+    M_SIM3P,        // SearchByProjection(KeyFrame*, Scw, ...)                 286-407
+    M_FUSE,         // Fuse(KeyFrame*, vector<MapPoint*>, th)                  1016-1134
+    M_FUSE_SCW,     // Fuse(KeyFrame*, Scw, vpPoints, th)                      1136-1265
+    M_SIM3,         // one direction of SearchBySim3                           1267-1505
+    M_BOW_KFF,      // SearchByBoW(KeyFrame*, Frame&)                          155-284
+    M_BOW_KFKF,     // SearchByBoW(KeyFrame*, KeyFrame*)                       715-850
+    M_TRIANG,       // SearchForTriangulation                                  852-1014
+};
+
+__host__ __device__ constexpr bool is_bow(int m) { return m == M_BOW_KFF || m == M_BOW_KFKF || m == M_TRIANG; }
+// candidate loop skips targets taken earlier in the same call -> sequential replay
+__host__ __device__ constexpr bool is_exclusive(int m) {
+    return m == M_LOCAL || m == M_WINDOW || m == M_F2F || m == M_MOTION || m == M_RELOC || m == M_SIM3P ||
+           m == M_BOW_KFF || m == M_BOW_KFKF || m == M_TRIANG;
+}
+// best and second best (ratio test) vs best only
+__host__ __device__ constexpr bool needs_second(int m) {
+    return m == M_LOCAL || m == M_WINDOW || m == M_F2F || m == M_BOW_KFF || m == M_BOW_KFKF;
+}
+
+// Target frame on the device.
+struct DView {
+    const orb_keypoint_t* kps;
+    const uint32_t* desc;  // n x 8
+    int n, nlevels;
+    int minX, maxX, minY, maxY;
+    float invW, invH;  // mfGridElementWidthInv / HeightInv (Frame.cc:77-78)
+    float sf[ORB_MAX_VIEW_LEVELS], sigma2[ORB_MAX_VIEW_LEVELS];
+    float fx, fy, cx, cy;
+    float R[9], t[3], Ow[3];
+    const int* cellStart;  // NCELLS + 1 (grid modes)
+    const int* items;      // grid: keypoint indices in traversal order; BoW: FV2 feature array
+};
+
+// Per-query window.  flags: 1 valid, 2 KeyFrame-style area (no level filter, <= r),
+// 4 post level filter [pMin, pMax] (KeyFrame matchers' kpLevel test)
+struct QP {
+    float u, v, r;
+    int flags;
+    int aMin, aMax;  // Frame::GetFeaturesInArea minLevel / maxLevel
+    int pMin, pMax;
+    int lo, hi;      // BoW: candidate range in DView::items
+};
+
+struct Job {
+    int mode;
+    DView T;
+    int qn;
+    const uint8_t* qflag;        // per query-side element: usable (TRIANG: has MapPoint)
+    const uint32_t* qdesc;       // query-side descriptor rows (x 8)
+    const orb_keypoint_t* qkps;  // query-side keypoints
+    const float* qpos;
+    const float* qnormal;
+    const float* qdmin;
+    const float* qdmax;
+    const float* qu;   // LOCAL: mTrackProjX; AREA: x
+    const float* qv;
+    const int* qlevel;  // LOCAL: mnTrackScaleLevel; AREA: (min, max) pairs
+    const float* qvcos;  // LOCAL: mTrackViewCos; AREA: r
+    float th, nnratio;
+    int window, minLevel, maxLevel, thDist, checkOri;
+    float SR[9], St[3];          // SIM3: sim transform applied after the source pose
+    float SRw[9], Stw[3];        // SIM3: source keyframe pose (R1w, t1w)
+    float qfx, qfy, qcx, qcy;    // SIM3: calibration of the projection (pKF1's)
+    float F12[9];
+    const uint8_t* tflag;        // BOW_KFKF: target usable; TRIANG: target has MapPoint
+    // BoW: query q = position in FV1's feature array
+    const uint32_t* fv1Nodes;
+    const int* fv1Off;
+    const int* fv1Feat;
+    int fv1N;
+    const uint32_t* fv2Nodes;
+    const int* fv2Off;
+    int fv2N;
+    // state, scratch, outputs
+    const uint8_t* taken0;  // T.n exclusion flags on entry (NULL = none)
+    QP* qp;
+    uint32_t* topk;  // qn x TOPK
+    int* cnt;        // qn
+    int* out;        // outN
+    int outN, outByTarget;
+    int* nOut;       // [0] = nmatches
+    int* areaOff;    // AREA fill: qn + 1 offsets
+    int* areaOut;
+};
+
+__device__ __forceinline__ int qrow(const Job& J, int q) { return is_bow(J.mode) ? J.fv1Feat[q] : q; }
+
+// ---- OpenCV 2.4 cv::Mat algebra on 3-vectors (oracle/ocv_ops.h states the semantics) ----
+__device__ __forceinline__ void gemm3_add(const float* A, const float* x, const float* t, float* o) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const float ti = A[3 * i] * x[0] + A[3 * i + 1] * x[1] + A[3 * i + 2] * x[2];
+        o[i] = (float)((double)ti * 1.0 + (double)t[i] * 1.0);
+    }
+}
+__device__ __forceinline__ double norm3(const float* v) {
+    double s = 0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const double e = v[i];
+        s += e * e;
+    }
+    return sqrt(s);
+}
+__device__ __forceinline__ double dot3(const float* a, const float* b) {
+    double r = 0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) r += (double)a[i] * (double)b[i];
+    return r;
+}
+__device__ __forceinline__ int predict_level(const DView& T, float ratio) {  // lower_bound, clamped
+    int n = 0;
+    while (n < T.nlevels && T.sf[n] < ratio) ++n;
+    return min(n, T.nlevels - 1);
+}
+__device__ __forceinline__ bool kf_in_image(const DView& T, float x, float y) {  // KeyFrame.cc:654-657
+    return x >= (float)T.minX && x < (float)T.maxX && y >= (float)T.minY && y < (float)T.maxY;
+}
+__device__ __forceinline__ int rot_bin(float a1, float a2) {  // ORBmatcher.cc:668-675
+    float rot = a1 - a2;
+    if (rot < 0.0f) rot += 360.0f;
+    int bin = (int)roundf(rot * (1.0f / HISTO));
+    if (bin == HISTO) bin = 0;
+    return bin;
+}
+__device__ __forceinline__ void load_desc(const uint32_t* p, uint32_t (&d)[8]) {
+    const uint4 a = *(const uint4*)p, b = *(const uint4*)(p + 4);
+    d[0] = a.x, d[1] = a.y, d[2] = a.z, d[3] = a.w, d[4] = b.x, d[5] = b.y, d[6] = b.z, d[7] = b.w;
+}
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
+    return v;
+}
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ void topk_insert(uint32_t (&t)[TOPK], uint32_t key) {
+#pragma unroll
+    for (int i = 0; i < TOPK; ++i) {
+        const uint32_t lo = min(t[i], key), hi = max(t[i], key);
+        t[i] = lo;
+        key = hi;
+    }
+}
+
+// ---- k_grid_build ------------------------------------------------------------------------
+// Frame::PosInGrid (Frame.cc:267-277) for every keypoint; CSR in cell order, keypoint order
+// inside a cell (the reference pushes back in index order, Frame.cc:117-123).
+__global__ void __launch_bounds__(1024) k_grid_build(const orb_keypoint_t* __restrict__ kps, int n, int minX,
+                                                     int minY, float invW, float invH, int* __restrict__ cellStart,
+                                                     int* __restrict__ items) {
+    __shared__ int s_cnt[NCELLS];
+    __shared__ int s_part[1024];
+    const int tid = threadIdx.x;
+    for (int c = tid; c < NCELLS; c += 1024) s_cnt[c] = 0;
+    __syncthreads();
+    for (int i = tid; i < n; i += 1024) {
+        const int px = (int)roundf((kps[i].x - (float)minX) * invW);
+        const int py = (int)roundf((kps[i].y - (float)minY) * invH);
+        if (!(px < 0 || px >= GRID_COLS || py < 0 || py >= GRID_ROWS)) atomicAdd(&s_cnt[px * GRID_ROWS + py], 1);
+    }
+    __syncthreads();
+    // exclusive scan: 3 cells per thread
+    const int c0 = tid * 3;
+    const int a = s_cnt[c0], b = s_cnt[c0 + 1], c = s_cnt[c0 + 2];
+    s_part[tid] = a + b + c;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const int v = tid >= o ? s_part[tid - o] : 0;
+        __syncthreads();
+        s_part[tid] += v;
+        __syncthreads();
+    }
+    const int base = s_part[tid] - (a + b + c);
+    cellStart[c0] = base;
+    cellStart[c0 + 1] = base + a;
+    cellStart[c0 + 2] = base + a + b;
+    if (tid == 1023) cellStart[NCELLS] = s_part[1023];
+    __syncthreads();
+    s_cnt[c0] = base;  // cursors
+    s_cnt[c0 + 1] = base + a;
+    s_cnt[c0 + 2] = base + a + b;
+    __syncthreads();
+    for (int i = tid; i < n; i += 1024) {
+        const int px = (int)roundf((kps[i].x - (float)minX) * invW);
+        const int py = (int)roundf((kps[i].y - (float)minY) * invH);
+        if (!(px < 0 || px >= GRID_COLS || py < 0 || py >= GRID_ROWS))
+            items[atomicAdd(&s_cnt[px * GRID_ROWS + py], 1)] = i;
+    }
+    __threadfence_block();
+    __syncthreads();
+    // restore index order inside each cell (cells hold a handful of keypoints)
+    for (int cc = tid; cc < NCELLS; cc += 1024) {
+        const int s = cellStart[cc], e = s_cnt[cc];
+        for (int i = s + 1; i < e; ++i) {
+            const int v = items[i];
+            int j = i - 1;
+            while (j >= s && items[j] > v) {
+                items[j + 1] = items[j];
+                --j;
+            }
+            items[j + 1] = v;
+        }
+    }
+}
+
+// ---- k_query_prep ------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_query_prep(Job J) {
+    const int q = blockIdx.x * 256 + threadIdx.x;
+    if (q >= J.qn) return;
+    const DView& T = J.T;
+    QP p;
+    p.u = p.v = p.r = 0.f;
+    p.flags = 0;
+    p.aMin = p.aMax = -1;
+    p.pMin = p.pMax = 0;
+    p.lo = p.hi = 0;
+    const int m = J.mode;
+    const int row = qrow(J, q);
+    bool ok = true;
+    if (m == M_TRIANG)
+        ok = !J.qflag[row];  // pMP1 -> continue (ORBmatcher.cc:895-897)
+    else if (J.qflag)
+        ok = J.qflag[row] != 0;
+    if (ok) switch (m) {
+            case M_AREA_F:
+            case M_AREA_KF:
+                p.u = J.qu[q];
+                p.v = J.qv[q];
+                p.r = J.qvcos[q];
+                p.aMin = J.qlevel ? J.qlevel[2 * q] : -1;
+                p.aMax = J.qlevel ? J.qlevel[2 * q + 1] : -1;
+                p.flags = 1 | (m == M_AREA_KF ? 2 : 0);
+                break;
+            case M_LOCAL: {  // ORBmatcher.cc:60-74 (+ RadiusByViewingCos 127-133)
+                const int pred = J.qlevel[q];
+                float r = (double)J.qvcos[q] > 0.998 ? 2.5f : 4.0f;
+                if (J.th != 1.0f) r *= J.th;
+                p.u = J.qu[q];
+                p.v = J.qv[q];
+                p.r = r * T.sf[pred];
+                p.aMin = pred - 1;
+                p.aMax = pred;
+                p.flags = 1;
+                break;
+            }
+            case M_WINDOW: {  // 427-446
+                const orb_keypoint_t kp1 = J.qkps[q];
+                const int level1 = kp1.octave;
+                if (J.minLevel > 0 && level1 < J.minLevel) break;
+                if (J.maxLevel < INT_MAX && level1 > J.maxLevel) break;
+                p.u = kp1.x;
+                p.v = kp1.y;
+                p.r = (float)J.window;
+                p.aMin = p.aMax = level1;
+                p.flags = 1;
+                break;
+            }
+            case M_F2F:      // 540-552
+            case M_MOTION:   // 1530-1551
+            case M_RELOC: {  // 1645-1673
+                float X[3];
+                gemm3_add(T.R, J.qpos + 3 * q, T.t, X);
+                const float xc = X[0], yc = X[1];
+                const float invzc = (float)(1.0 / (double)X[2]);
+                const float u = __builtin_fmaf(T.fx * xc, invzc, T.cx);
+                const float v = __builtin_fmaf(T.fy * yc, invzc, T.cy);
+                p.u = u;
+                p.v = v;
+                if (m == M_F2F) {
+                    const int level1 = J.qkps[q].octave;
+                    p.r = (float)J.window;
+                    p.aMin = p.aMax = level1;
+                    p.flags = 1;
+                    break;
+                }
+                if (u < (float)T.minX || u > (float)T.maxX) break;
+                if (v < (float)T.minY || v > (float)T.maxY) break;
+                if (m == M_MOTION) {
+                    const int oct = J.qkps[q].octave;
+                    p.r = J.th * T.sf[oct];
+                    p.aMin = oct - 1;
+                    p.aMax = oct + 1;
+                } else {
+                    float PO[3];
+                    const float* P = J.qpos + 3 * q;
+                    PO[0] = P[0] - T.Ow[0];
+                    PO[1] = P[1] - T.Ow[1];
+                    PO[2] = P[2] - T.Ow[2];
+                    const float dist3D = (float)norm3(PO);
+                    const float ratio = dist3D / J.qdmin[q];
+                    const int pred = predict_level(T, ratio);
+                    p.r = J.th * T.sf[pred];
+                    p.aMin = pred - 1;
+                    p.aMax = pred + 1;
+                }
+                p.flags = 1;
+                break;
+            }
+            case M_SIM3P:      // 310-366
+            case M_FUSE:       // 1038-1089
+            case M_FUSE_SCW: {  // 1161-1212
+                const float* P = J.qpos + 3 * q;
+                float X[3];
+                gemm3_add(T.R, P, T.t, X);
+                if (X[2] < 0.0f) break;
+                const float invz = m == M_FUSE_SCW ? (float)(1.0 / (double)X[2]) : 1.0f / X[2];
+                const float x = X[0] * invz, y = X[1] * invz;
+                const float u = __builtin_fmaf(T.fx, x, T.cx), v = __builtin_fmaf(T.fy, y, T.cy);
+                if (!kf_in_image(T, u, v)) break;
+                float PO[3] = {P[0] - T.Ow[0], P[1] - T.Ow[1], P[2] - T.Ow[2]};
+                const float dist3D = (float)norm3(PO);
+                const float minDistance = J.qdmin[q], maxDistance = J.qdmax[q];
+                if (dist3D < minDistance || dist3D > maxDistance) break;
+                if (dot3(PO, J.qnormal + 3 * q) < 0.5 * (double)dist3D) break;
+                const float ratio = dist3D / minDistance;
+                const int pred = predict_level(T, ratio);
+                p.u = u;
+                p.v = v;
+                p.r = J.th * T.sf[pred];
+                p.pMin = pred - 1;
+                p.pMax = pred;
+                p.flags = 1 | 2 | 4;
+                break;
+            }
+            case M_SIM3: {  // 1321-1367 / 1391-1437
+                float X1[3], X2[3];
+                gemm3_add(J.SRw, J.qpos + 3 * q, J.Stw, X1);
+                gemm3_add(J.SR, X1, J.St, X2);
+                if (X2[2] < 0.0f) break;
+                const float invz = (float)(1.0 / (double)X2[2]);
+                const float x = X2[0] * invz, y = X2[1] * invz;
+                const float u = __builtin_fmaf(J.qfx, x, J.qcx), v = __builtin_fmaf(J.qfy, y, J.qcy);
+                if (!kf_in_image(T, u, v)) break;
+                const float dist3D = (float)norm3(X2);
+                const float minDistance = J.qdmin[q], maxDistance = J.qdmax[q];
+                if (dist3D < minDistance || dist3D > maxDistance) break;
+                const float ratio = dist3D / minDistance;
+                const int pred = predict_level(T, ratio);
+                p.u = u;
+                p.v = v;
+                p.r = J.th * T.sf[pred];
+                p.pMin = pred - 1;
+                p.pMax = pred;
+                p.flags = 1 | 2 | 4;
+                break;
+            }
+            default: {  // BoW: the FeatureVector merge walk (ORBmatcher.cc:177-262) visits the
+                // nodes present in both vectors in ascending id order
+                int a = 0, hi = J.fv1N;
+                while (a < hi) {  // node of position q: last a with fv1Off[a] <= q
+                    const int mid = (a + hi) >> 1;
+                    if (J.fv1Off[mid + 1] <= q)
+                        a = mid + 1;
+                    else
+                        hi = mid;
+                }
+                const uint32_t id = J.fv1Nodes[a];
+                int lo2 = 0, hi2 = J.fv2N;
+                while (lo2 < hi2) {
+                    const int mid = (lo2 + hi2) >> 1;
+                    if (J.fv2Nodes[mid] < id)
+                        lo2 = mid + 1;
+                    else
+                        hi2 = mid;
+                }
+                if (lo2 < J.fv2N && J.fv2Nodes[lo2] == id) {
+                    p.lo = J.fv2Off[lo2];
+                    p.hi = J.fv2Off[lo2 + 1];
+                    p.flags = 1;
+                }
+                break;
+            }
+        }
+    J.qp[q] = p;
+}
+
+// ---- candidate enumeration (one wave, lanes stride the candidates in traversal order) ----
+// visit(pos, idx): `pos` is monotone in the reference's candidate order.
+template <class V>
+__device__ __forceinline__ void enum_candidates(const Job& J, const QP& p, int lane, V&& visit) {
+    const DView& T = J.T;
+    if (is_bow(J.mode)) {
+        for (int pos = p.lo + lane; pos < p.hi; pos += 64) visit(pos, T.items[pos]);
+        return;
+    }
+    // Frame.cc:205-223 / KeyFrame.cc:617-635
+    int minCX = (int)floorf((p.u - (float)T.minX - p.r) * T.invW);
+    minCX = max(0, minCX);
+    if (minCX >= GRID_COLS) return;
+    int maxCX = (int)ceilf((p.u - (float)T.minX + p.r) * T.invW);
+    maxCX = min(GRID_COLS - 1, maxCX);
+    if (maxCX < 0) return;
+    int minCY = (int)floorf((p.v - (float)T.minY - p.r) * T.invH);
+    minCY = max(0, minCY);
+    if (minCY >= GRID_ROWS) return;
+    int maxCY = (int)ceilf((p.v - (float)T.minY + p.r) * T.invH);
+    maxCY = min(GRID_ROWS - 1, maxCY);
+    if (maxCY < 0) return;
+    const bool kfArea = p.flags & 2, post = p.flags & 4;
+    const bool checkLevels = !(p.aMin == -1 && p.aMax == -1), sameLevel = checkLevels && p.aMin == p.aMax;
+    for (int ix = minCX; ix <= maxCX; ++ix) {
+        const int lo = T.cellStart[ix * GRID_ROWS + minCY], hi = T.cellStart[ix * GRID_ROWS + maxCY + 1];
+        for (int pos = lo + lane; pos < hi; pos += 64) {
+            const int idx = T.items[pos];
+            const orb_keypoint_t kp = T.kps[idx];
+            if (kfArea) {
+                if (!(fabsf(kp.x - p.u) <= p.r && fabsf(kp.y - p.v) <= p.r)) continue;
+                if (post && (kp.octave < p.pMin || kp.octave > p.pMax)) continue;
+            } else {
+                if (checkLevels && !sameLevel) {
+                    if (kp.octave < p.aMin || kp.octave > p.aMax) continue;
+                } else if (sameLevel) {
+                    if (kp.octave != p.aMin) continue;
+                }
+                if (fabsf(kp.x - p.u) > p.r || fabsf(kp.y - p.v) > p.r) continue;
+            }
+            visit(pos, idx);
+        }
+    }
+}
+
+// Candidate key: (distance << 16) | order; order = traversal position, or the target index
+// for SearchForTriangulation (its vDistIndex is sorted by (dist, idx2), ORBmatcher.cc:926).
+__device__ __forceinline__ uint32_t cand_key(int mode, int dist, int pos, int idx) {
+    return ((uint32_t)dist << 16) | (uint32_t)(mode == M_TRIANG ? idx : pos);
+}
+__device__ __forceinline__ int key_idx(const Job& J, uint32_t key) {
+    return J.mode == M_TRIANG ? (int)(key & 0xFFFF) : J.T.items[key & 0xFFFF];
+}
+
+// ---- k_query_scan: one wave per query ---------------------------------------------------
+__global__ void __launch_bounds__(256) k_query_scan(Job J) {
+    const int q = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (q >= J.qn) return;
+    const QP p = J.qp[q];
+    int n = 0;
+    uint32_t top[TOPK];
+#pragma unroll
+    for (int k = 0; k < TOPK; ++k) top[k] = 0xFFFFFFFFu;
+    if (p.flags & 1) {
+        if (J.mode == M_AREA_F || J.mode == M_AREA_KF) {
+            enum_candidates(J, p, lane, [&](int, int) { ++n; });
+            n = wave_sum(n);
+            if (lane == 0) J.cnt[q] = n;
+            return;
+        }
+        uint32_t d1[8];
+        load_desc(J.qdesc + (size_t)qrow(J, q) * 8, d1);
+        const int m = J.mode;
+        enum_candidates(J, p, lane, [&](int pos, int idx) {
+            if (J.taken0 && J.taken0[idx]) return;
+            if (m == M_BOW_KFKF && !J.tflag[idx]) return;  // !pMP2 || isBad (768-772)
+            if (m == M_TRIANG && J.tflag[idx]) return;     // pMP2 (905-907)
+            uint32_t d2[8];
+            load_desc(J.T.desc + (size_t)idx * 8, d2);
+            const int dist = hamming256(d1, d2);
+            if (m == M_TRIANG && dist > TH_LOW) return;  // (913-914)
+            topk_insert(top, cand_key(m, dist, pos, idx));
+            ++n;
+        });
+    }
+    n = wave_sum(n);
+    // merge the lanes' sorted lists: 8 rounds of wave-min; keys are unique per candidate
+    uint32_t res = 0xFFFFFFFFu;
+#pragma unroll
+    for (int k = 0; k < TOPK; ++k) {
+        const uint32_t mn = wave_min(top[0]);
+        if (top[0] == mn && mn != 0xFFFFFFFFu) {
+#pragma unroll
+            for (int i = 0; i < TOPK - 1; ++i) top[i] = top[i + 1];
+            top[TOPK - 1] = 0xFFFFFFFFu;
+        }
+        if (lane == k) res = mn;
+    }
+    if (lane < TOPK) J.topk[(size_t)q * TOPK + lane] = res;
+    if (lane == 0) J.cnt[q] = n;
+}
+
+// AREA: ordered write of every candidate index (wave per query, ballot compaction)
+__global__ void __launch_bounds__(256) k_area_fill(Job J) {
+    const int q = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (q >= J.qn) return;
+    const QP p = J.qp[q];
+    if (!(p.flags & 1)) return;
+    const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    int base = J.areaOff[q];
+    // enum_candidates visits in strided lane order; wrap each 64-candidate batch of a cell
+    // range with a ballot so the output keeps the traversal order
+    const DView& T = J.T;
+    int minCX = (int)floorf((p.u - (float)T.minX - p.r) * T.invW);
+    minCX = max(0, minCX);
+    if (minCX >= GRID_COLS) return;
+    int maxCX = (int)ceilf((p.u - (float)T.minX + p.r) * T.invW);
+    maxCX = min(GRID_COLS - 1, maxCX);
+    if (maxCX < 0) return;
+    int minCY = (int)floorf((p.v - (float)T.minY - p.r) * T.invH);
+    minCY = max(0, minCY);
+    if (minCY >= GRID_ROWS) return;
+    int maxCY = (int)ceilf((p.v - (float)T.minY + p.r) * T.invH);
+    maxCY = min(GRID_ROWS - 1, maxCY);
+    if (maxCY < 0) return;
+    const bool kfArea = p.flags & 2;
+    const bool checkLevels = !(p.aMin == -1 && p.aMax == -1), sameLevel = checkLevels && p.aMin == p.aMax;
+    for (int ix = minCX; ix <= maxCX; ++ix) {
+        const int lo = T.cellStart[ix * GRID_ROWS + minCY], hi = T.cellStart[ix * GRID_ROWS + maxCY + 1];
+        for (int p0 = lo; p0 < hi; p0 += 64) {
+            const int pos = p0 + lane;
+            bool keep = false;
+            int idx = 0;
+            if (pos < hi) {
+                idx = T.items[pos];
+                const orb_keypoint_t kp = T.kps[idx];
+                if (kfArea) {
+                    keep = fabsf(kp.x - p.u) <= p.r && fabsf(kp.y - p.v) <= p.r;
+                } else {
+                    keep = true;
+                    if (checkLevels && !sameLevel) {
+                        if (kp.octave < p.aMin || kp.octave > p.aMax) keep = false;
+                    } else if (sameLevel) {
+                        if (kp.octave != p.aMin) keep = false;
+                    }
+                    if (fabsf(kp.x - p.u) > p.r || fabsf(kp.y - p.v) > p.r) keep = false;
+                }
+            }
+            const uint64_t m = __ballot(keep);
+            if (keep) J.areaOut[base + __popcll(m & below)] = idx;
+            base += __popcll(m);
+        }
+    }
+}
+
+// ---- k_resolve -------------------------------------------------------------------------
+// Exact rescan of query q against the live taken flags: the two smallest keys.
+__device__ void rescan_best2(const Job& J, int q, const QP& p, const uint8_t* s_taken, int lane, uint32_t* b1,
+                             uint32_t* b2) {
+    uint32_t d1[8];
+    load_desc(J.qdesc + (size_t)qrow(J, q) * 8, d1);
+    uint32_t lb = 0xFFFFFFFFu, ls = 0xFFFFFFFFu;
+    const int m = J.mode;
+    enum_candidates(J, p, lane, [&](int pos, int idx) {
+        if (s_taken[idx]) return;
+        if (m == M_BOW_KFKF && !J.tflag[idx]) return;
+        if (m == M_TRIANG && J.tflag[idx]) return;
+        uint32_t d2[8];
+        load_desc(J.T.desc + (size_t)idx * 8, d2);
+        const int dist = hamming256(d1, d2);
+        if (m == M_TRIANG && dist > TH_LOW) return;
+        const uint32_t key = cand_key(m, dist, pos, idx);
+        if (key < lb) {
+            ls = lb;
+            lb = key;
+        } else if (key < ls) {
+            ls = key;
+        }
+    });
+    const uint32_t g1 = wave_min(lb);
+    const uint32_t g2 = wave_min(lb == g1 ? ls : lb);
+    *b1 = g1;
+    *b2 = g2;
+}
+
+// SearchForTriangulation rescan: smallest untaken key with dist <= DistTh passing the
+// epipolar test (the first such entry of the sorted vDistIndex walk, ORBmatcher.cc:926-955).
+__device__ __forceinline__ bool epipolar_ok(const Job& J, const orb_keypoint_t& kp1, const orb_keypoint_t& kp2) {
+    // CheckDistEpipolarLine (ORBmatcher.cc:136-153), g++ -O3 -march=native contraction
+    const float* F = J.F12;
+    const float a = __builtin_fmaf(kp1.x, F[0], kp1.y * F[3]) + F[6];
+    const float b = __builtin_fmaf(kp1.x, F[1], kp1.y * F[4]) + F[7];
+    const float c = __builtin_fmaf(kp1.y, F[5], kp1.x * F[2]) + F[8];
+    const float num = __builtin_fmaf(b, kp2.y, a * kp2.x) + c;
+    const float den = __builtin_fmaf(a, a, b * b);
+    if (den == 0) return false;
+    const float dsqr = num * num / den;
+    return (double)dsqr < 3.84 * (double)J.T.sigma2[kp2.octave];
+}
+
+__device__ uint32_t triang_rescan(const Job& J, int q, const QP& p, const uint8_t* s_taken, int lane) {
+    uint32_t b1, b2;
+    rescan_best2(J, q, p, s_taken, lane, &b1, &b2);
+    if (b1 == 0xFFFFFFFFu) return 0xFFFFFFFFu;
+    const int distTh = 2 * (int)(b1 >> 16);
+    const orb_keypoint_t kp1 = J.qkps[qrow(J, q)];
+    uint32_t d1[8];
+    load_desc(J.qdesc + (size_t)qrow(J, q) * 8, d1);
+    uint32_t best = 0xFFFFFFFFu;
+    enum_candidates(J, p, lane, [&](int pos, int idx) {
+        if (s_taken[idx] || J.tflag[idx]) return;
+        uint32_t d2[8];
+        load_desc(J.T.desc + (size_t)idx * 8, d2);
+        const int dist = hamming256(d1, d2);
+        if (dist > TH_LOW || dist > distTh) return;
+        const uint32_t key = cand_key(M_TRIANG, dist, pos, idx);
+        if (key < best && epipolar_ok(J, kp1, J.T.kps[idx])) best = key;
+    });
+    return wave_min(best);
+}
+
+__global__ void __launch_bounds__(256) k_resolve(Job J) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ int s_hist[HISTO + 2];
+    __shared__ int s_ind[3];
+    __shared__ int s_nacc;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int Tn = J.T.n, m = J.mode;
+    int* s_out = (int*)smem;                                  // outN
+    int* s_acc = s_out + J.outN;                               // accepted: (slot << 5) | bin
+    uint8_t* s_taken = (uint8_t*)(s_acc + max(Tn, 1));          // Tn
+    for (int i = tid; i < J.outN; i += 256) s_out[i] = -1;
+    for (int i = tid; i < Tn; i += 256) s_taken[i] = J.taken0 ? J.taken0[i] : 0;
+    if (tid == 0) s_nacc = 0;
+    __syncthreads();
+    const bool rotMode = J.checkOri && (m == M_WINDOW || m == M_MOTION || m == M_RELOC || m == M_BOW_KFF ||
+                                        m == M_BOW_KFKF || m == M_TRIANG);
+    if (!is_exclusive(m)) {
+        // Fuse / SearchBySim3: best distance per query, no cross-query state
+        int acc = 0;
+        for (int q = tid; q < J.qn; q += 256) {
+            if (!(J.qp[q].flags & 1) || J.cnt[q] == 0) continue;
+            const uint32_t e = J.topk[(size_t)q * TOPK];
+            const int dist = (int)(e >> 16);
+            if (dist <= J.thDist) {
+                s_out[q] = key_idx(J, e);
+                ++acc;
+            }
+        }
+        atomicAdd(&s_nacc, acc);
+    } else if (wave == 0) {
+        int nacc = 0;
+        for (int q = 0; q < J.qn; ++q) {
+            const QP p = J.qp[q];
+            if (!(p.flags & 1)) continue;
+            const int cnt = J.cnt[q];
+            if (cnt == 0) continue;
+            const int k = min(cnt, TOPK);
+            const uint32_t e = lane < k ? J.topk[(size_t)q * TOPK + lane] : 0xFFFFFFFFu;
+            const int eidx = lane < k ? key_idx(J, e) : 0;
+            const bool untaken = lane < k && !s_taken[eidx];
+            const uint64_t um = __ballot(untaken);
+            int bestIdx = -1, bestDist = INT_MAX, bestDist2 = INT_MAX, bestLevel = -1, bestLevel2 = -1;
+            if (m == M_TRIANG) {
+                // walk the sorted list: BestDist from the first untaken entry, then the first
+                // untaken entry within round(2*BestDist) that passes the epipolar test
+                uint32_t chosen = 0xFFFFFFFFu;
+                bool decided = false;
+                if (um != 0ull) {
+                    const int first = __ffsll((unsigned long long)um) - 1;
+                    const int distTh = 2 * (int)(__shfl(e, first, 64) >> 16);
+                    const orb_keypoint_t kp1 = J.qkps[qrow(J, q)];
+                    const bool inTh = lane < k && (int)(e >> 16) <= distTh;
+                    const bool pass = untaken && inTh && epipolar_ok(J, kp1, J.T.kps[eidx]);
+                    const uint64_t pm = __ballot(pass), om = __ballot(lane < k && !inTh);
+                    if (pm != 0ull) {
+                        chosen = __shfl(e, __ffsll((unsigned long long)pm) - 1, 64);
+                        decided = true;
+                    } else if (om != 0ull || cnt <= TOPK) {
+                        decided = true;  // the walk breaks on an entry past DistTh, or ends
+                    }
+                } else if (cnt <= TOPK) {
+                    decided = true;
+                }
+                if (!decided) chosen = triang_rescan(J, q, p, s_taken, lane);
+                if (chosen == 0xFFFFFFFFu) continue;
+                bestIdx = key_idx(J, chosen);
+                bestDist = 0;  // accepted below unconditionally
+            } else {
+                const int need = needs_second(m) ? 2 : 1;
+                uint32_t b1 = 0xFFFFFFFFu, b2 = 0xFFFFFFFFu;
+                if (__popcll(um) >= need || cnt <= TOPK) {
+                    if (um != 0ull) {
+                        b1 = __shfl(e, __ffsll((unsigned long long)um) - 1, 64);
+                        const uint64_t um2 = um & (um - 1);
+                        if (um2) b2 = __shfl(e, __ffsll((unsigned long long)um2) - 1, 64);
+                    }
+                } else {
+                    rescan_best2(J, q, p, s_taken, lane, &b1, &b2);
+                }
+                if (b1 == 0xFFFFFFFFu) continue;  // every candidate taken: bestDist stays INT_MAX
+                bestIdx = key_idx(J, b1);
+                bestDist = (int)(b1 >> 16);
+                bestLevel = J.T.kps[bestIdx].octave;
+                if (b2 != 0xFFFFFFFFu) {
+                    bestDist2 = (int)(b2 >> 16);
+                    bestLevel2 = J.T.kps[key_idx(J, b2)].octave;
+                }
+            }
+            bool accept = false;
+            switch (m) {
+                case M_LOCAL:  // 112-121
+                    accept = bestDist <= TH_HIGH &&
+                             !(bestLevel == bestLevel2 && (float)bestDist > J.nnratio * (float)bestDist2);
+                    break;
+                case M_WINDOW:  // 476
+                case M_F2F:     // 585
+                    accept = (float)bestDist <= (float)bestDist2 * J.nnratio && bestDist <= TH_HIGH;
+                    break;
+                case M_BOW_KFF:  // 222-226
+                    accept = bestDist <= TH_LOW && (float)bestDist < J.nnratio * (float)bestDist2;
+                    break;
+                case M_BOW_KFKF:  // 789-793
+                    accept = bestDist < TH_LOW && (float)bestDist < J.nnratio * (float)bestDist2;
+                    break;
+                case M_MOTION:  // 1576
+                    accept = bestDist <= TH_HIGH;
+                    break;
+                case M_RELOC:  // 1701
+                case M_SIM3P:  // 393
+                    accept = bestDist <= J.thDist;
+                    break;
+                case M_TRIANG:
+                    accept = true;
+                    break;
+                default:
+                    break;
+            }
+            if (!accept) continue;
+            if (lane == 0) {
+                s_taken[bestIdx] = 1;
+                const int qv = qrow(J, q);
+                const int slot = J.outByTarget ? bestIdx : qv;
+                s_out[slot] = J.outByTarget ? qv : bestIdx;
+                if (rotMode) {
+                    const float a1 = J.qkps[qv].angle, a2 = J.T.kps[bestIdx].angle;
+                    s_acc[nacc] = (slot << 5) | rot_bin(a1, a2);
+                }
+            }
+            ++nacc;
+            // lane 0's LDS writes land before any lane's next read (same wave, in order)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        if (lane == 0) s_nacc = nacc;
+    }
+    __syncthreads();
+    int removed = 0;
+    if (rotMode && is_exclusive(m)) {  // rotation consistency (e.g. ORBmatcher.cc:491-512)
+        const int nacc = s_nacc;
+        if (tid < HISTO) s_hist[tid] = 0;
+        __syncthreads();
+        for (int i = tid; i < nacc; i += 256) atomicAdd(&s_hist[s_acc[i] & 31], 1);
+        __syncthreads();
+        if (tid == 0) {  // ComputeThreeMaxima (1748-1789)
+            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+            for (int i = 0; i < HISTO; ++i) {
+                const int sz = s_hist[i];
+                if (sz > max1) {
+                    max3 = max2;
+                    max2 = max1;
+                    max1 = sz;
+                    ind3 = ind2;
+                    ind2 = ind1;
+                    ind1 = i;
+                } else if (sz > max2) {
+                    max3 = max2;
+                    max2 = sz;
+                    ind3 = ind2;
+                    ind2 = i;
+                } else if (sz > max3) {
+                    max3 = sz;
+                    ind3 = i;
+                }
+            }
+            if (max2 < 0.1f * (float)max1) {
+                ind2 = -1;
+                ind3 = -1;
+            } else if (max3 < 0.1f * (float)max1) {
+                ind3 = -1;
+            }
+            s_ind[0] = ind1;
+            s_ind[1] = ind2;
+            s_ind[2] = ind3;
+        }
+        __syncthreads();
+        for (int i = tid; i < nacc; i += 256) {
+            const int b = s_acc[i] & 31;
+            if (b != s_ind[0] && b != s_ind[1] && b != s_ind[2]) {
+                s_out[s_acc[i] >> 5] = -1;
+                ++removed;
+            }
+        }
+    }
+    removed = wave_sum(removed);
+    __syncthreads();
+    if (lane == 0 && removed) atomicAdd(&s_nacc, -removed);
+    __syncthreads();
+    for (int i = tid; i < J.outN; i += 256) J.out[i] = s_out[i];
+    if (tid == 0) J.nOut[0] = s_nacc;
+}
+
+// SearchBySim3 agreement (ORBmatcher.cc:1489-1502): match12[i1] = idx2 iff vnMatch2[idx2] == i1.
+__global__ void k_sim3_agree(const int* __restrict__ m1, int n1, const int* __restrict__ m2, int* __restrict__ out,
+                             int* __restrict__ nOut) {
+    __shared__ int s_n;
+    if (threadIdx.x == 0) s_n = 0;
+    __syncthreads();
+    int c = 0;
+    for (int i = threadIdx.x; i < n1; i += blockDim.x) {
+        const int idx2 = m1[i];
+        const bool ok = idx2 >= 0 && m2[idx2] == i;
+        out[i] = ok ? idx2 : -1;
+        c += ok;
+    }
+    atomicAdd(&s_n, c);
+    __syncthreads();
+    if (threadIdx.x == 0) nOut[0] = s_n;
+}
+
+// =========================================================================================
+// host side
+// =========================================================================================
+int fail(int code, const std::string& msg) { return orb_internal_set_error(code, msg); }
+
+// Per-device arena + stream; host entry points are synchronous and serialised per device.
+struct DeviceCtx {
+    std::mutex mu;
+    hipStream_t stream = nullptr;
+    uint8_t* buf = nullptr;
+    size_t cap = 0;
+    uint8_t* pinned = nullptr;  // host staging
+    size_t pcap = 0;
+};
+DeviceCtx g_ctx[64];
+
+// Bump allocator over one device buffer; `stage` copies a host array into it.
+struct Arena {
+    std::vector<std::pair<size_t, std::pair<const void*, size_t>>> uploads;
+    size_t size = 0;
+    size_t take(size_t bytes) {
+        const size_t off = size;
+        size += (bytes + 255) & ~(size_t)255;
+        return off;
+    }
+    size_t stage(const void* host, size_t bytes) {
+        const size_t off = take(bytes ? bytes : 1);
+        if (host && bytes) uploads.push_back({off, {host, bytes}});
+        return off;
+    }
+};
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        hipGetDevice(&prev);
+        hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) hipSetDevice(prev);
+    }
+};
+
+#define HIPCHK(expr)                                                                          \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess) return fail(ORB_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+// A call in flight: the arena layout is planned first (offsets), then allocated + uploaded.
+struct Call {
+    int device;
+    DeviceCtx* ctx = nullptr;
+    Arena A;
+    uint8_t* base = nullptr;
+    template <class T>
+    T* at(size_t off) const {
+        return (T*)(base + off);
+    }
+    int begin() {
+        if (device < 0 || device >= 64) return fail(ORB_EINVAL, "bad device ordinal");
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || device >= n) return fail(ORB_EINVAL, "no such HIP device");
+        ctx = &g_ctx[device];
+        return ORB_OK;
+    }
+    // allocate (grow) the arena and upload every staged array in one H2D copy
+    int commit() {
+        if (!ctx->stream) HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+        if (A.size > ctx->cap) {
+            const size_t want = std::max(A.size, ctx->cap * 2);
+            if (ctx->buf) hipFree(ctx->buf);
+            ctx->buf = nullptr;
+            ctx->cap = 0;
+            HIPCHK(hipMalloc(&ctx->buf, want));
+            ctx->cap = want;
+        }
+        if (A.size > ctx->pcap) {
+            if (ctx->pinned) hipHostFree(ctx->pinned);
+            ctx->pinned = nullptr;
+            ctx->pcap = 0;
+            HIPCHK(hipHostMalloc((void**)&ctx->pinned, A.size, hipHostMallocDefault));
+            ctx->pcap = A.size;
+        }
+        base = ctx->buf;
+        size_t hi = 0;
+        for (auto& u : A.uploads) {
+            std::memcpy(ctx->pinned + u.first, u.second.first, u.second.second);
+            hi = std::max(hi, u.first + u.second.second);
+        }
+        if (hi) HIPCHK(hipMemcpyAsync(base, ctx->pinned, hi, hipMemcpyHostToDevice, ctx->stream));
+        return ORB_OK;
+    }
+    int download(void* host, size_t off, size_t bytes) {
+        if (bytes) HIPCHK(hipMemcpyAsync(host, base + off, bytes, hipMemcpyDeviceToHost, ctx->stream));
+        return ORB_OK;
+    }
+    int sync() {
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        return ORB_OK;
+    }
+};
+
+int check_view(const orb_frame_view_t* v, const char* name) {
+    if (!v) return fail(ORB_EINVAL, std::string(name) + ": NULL view");
+    if (v->n < 0 || v->n > MAX_TARGET) return fail(ORB_ENOTSUP, std::string(name) + ": keypoint count out of range");
+    if (v->n > 0 && (!v->kps || !v->desc)) return fail(ORB_EINVAL, std::string(name) + ": NULL keypoints/descriptors");
+    if (v->nlevels < 1 || v->nlevels > ORB_MAX_VIEW_LEVELS)
+        return fail(ORB_EINVAL, std::string(name) + ": nlevels out of range");
+    if (v->bounds.max_x <= v->bounds.min_x || v->bounds.max_y <= v->bounds.min_y)
+        return fail(ORB_EINVAL, std::string(name) + ": bad bounds");
+    for (int i = 0; i < v->n; ++i)
+        if (v->kps[i].octave < 0 || v->kps[i].octave >= v->nlevels)
+            return fail(ORB_EINVAL, std::string(name) + ": keypoint octave out of range");
+    return ORB_OK;
+}
+
+// Offsets of a target view inside the arena.
+struct ViewOffs {
+    size_t kps, desc, cellStart, items;
+};
+
+ViewOffs plan_view(Arena& A, const orb_frame_view_t* v, bool grid) {
+    ViewOffs o{};
+    o.kps = A.stage(v->kps, (size_t)v->n * sizeof(orb_keypoint_t));
+    o.desc = A.stage(v->desc, (size_t)v->n * 32);
+    if (grid) {
+        o.cellStart = A.take((NCELLS + 1) * sizeof(int));
+        o.items = A.take((size_t)std::max(v->n, 1) * sizeof(int));
+    }
+    return o;
+}
+
+DView make_dview(const Call& C, const orb_frame_view_t* v, const ViewOffs& o, bool grid) {
+    DView d{};
+    d.kps = C.at<orb_keypoint_t>(o.kps);
+    d.desc = C.at<uint32_t>(o.desc);
+    d.n = v->n;
+    d.nlevels = v->nlevels;
+    d.minX = v->bounds.min_x;
+    d.maxX = v->bounds.max_x;
+    d.minY = v->bounds.min_y;
+    d.maxY = v->bounds.max_y;
+    d.invW = static_cast<float>(GRID_COLS) / static_cast<float>(v->bounds.max_x - v->bounds.min_x);
+    d.invH = static_cast<float>(GRID_ROWS) / static_cast<float>(v->bounds.max_y - v->bounds.min_y);
+    std::memcpy(d.sf, v->scale_factors, sizeof(d.sf));
+    std::memcpy(d.sigma2, v->level_sigma2, sizeof(d.sigma2));
+    d.fx = v->fx;
+    d.fy = v->fy;
+    d.cx = v->cx;
+    d.cy = v->cy;
+    std::memcpy(d.R, v->Rcw, sizeof(d.R));
+    std::memcpy(d.t, v->tcw, sizeof(d.t));
+    std::memcpy(d.Ow, v->Ow, sizeof(d.Ow));
+    if (grid) {
+        d.cellStart = C.at<int>(o.cellStart);
+        d.items = C.at<int>(o.items);
+    }
+    return d;
+}
+
+int launch_grid(const Call& C, const DView& d) {
+    hipLaunchKernelGGL(k_grid_build, dim3(1), dim3(1024), 0, C.ctx->stream, d.kps, d.n, d.minX, d.minY, d.invW,
+                       d.invH, (int*)d.cellStart, (int*)d.items);
+    HIPCHK(hipGetLastError());
+    return ORB_OK;
+}
+
+// Scratch of a job: qp, topk, cnt (+ outputs).
+struct JobOffs {
+    size_t qp, topk, cnt, out, nOut;
+};
+JobOffs plan_job(Arena& A, int qn, int outN) {
+    JobOffs o{};
+    o.qp = A.take((size_t)std::max(qn, 1) * sizeof(QP));
+    o.topk = A.take((size_t)std::max(qn, 1) * TOPK * 4);
+    o.cnt = A.take((size_t)std::max(qn, 1) * 4);
+    o.out = A.take((size_t)std::max(outN, 1) * 4);
+    o.nOut = A.take(16);
+    return o;
+}
+void bind_job(const Call& C, Job& J, const JobOffs& o, int qn, int outN) {
+    J.qn = qn;
+    J.qp = C.at<QP>(o.qp);
+    J.topk = C.at<uint32_t>(o.topk);
+    J.cnt = C.at<int>(o.cnt);
+    J.out = C.at<int>(o.out);
+    J.outN = outN;
+    J.nOut = C.at<int>(o.nOut);
+}
+
+int resolve_lds(const Job& J, size_t* bytes) {
+    *bytes = (size_t)J.outN * 4 + (size_t)std::max(J.T.n, 1) * 4 + (size_t)J.T.n + 16;
+    if (*bytes > 150 * 1024) return fail(ORB_ENOTSUP, "matcher state exceeds LDS (too many keypoints/queries)");
+    return ORB_OK;
+}
+
+int run_job(const Call& C, const Job& J) {
+    hipStream_t s = C.ctx->stream;
+    if (J.qn > 0) {
+        hipLaunchKernelGGL(k_query_prep, dim3((J.qn + 255) / 256), dim3(256), 0, s, J);
+        hipLaunchKernelGGL(k_query_scan, dim3((J.qn + 3) / 4), dim3(256), 0, s, J);
+    }
+    size_t lds = 0;
+    int st = resolve_lds(J, &lds);
+    if (st) return st;
+    static bool attr_set[64] = {};
+    if (!attr_set[C.device]) {
+        HIPCHK(hipFuncSetAttribute((const void*)k_resolve, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
+        attr_set[C.device] = true;
+    }
+    hipLaunchKernelGGL(k_resolve, dim3(1), dim3(256), lds, s, J);
+    HIPCHK(hipGetLastError());
+    return ORB_OK;
+}
+
+Job base_job(int mode) {
+    Job J;
+    std::memset(&J, 0, sizeof(J));
+    J.mode = mode;
+    J.nnratio = 0.6f;
+    J.th = 1.0f;
+    J.thDist = TH_HIGH;
+    return J;
+}
+
+bool bad_fv(const orb_feature_vector_t& f, int n) {
+    if (f.n_nodes < 0) return true;
+    if (f.n_nodes == 0) return false;
+    if (!f.nodes || !f.offsets || !f.features || f.offsets[0] != 0) return true;
+    for (int a = 0; a < f.n_nodes; ++a) {
+        if (f.offsets[a + 1] < f.offsets[a]) return true;
+        if (a && f.nodes[a] <= f.nodes[a - 1]) return true;
+    }
+    for (int i = 0; i < f.offsets[f.n_nodes]; ++i)
+        if (f.features[i] < 0 || f.features[i] >= n) return true;
+    return f.offsets[f.n_nodes] > 65535;
+}
+
+// Shared driver of the three BoW matchers.
+int bow_match(int mode, const orb_frame_view_t* V1, const uint8_t* flag1, orb_feature_vector_t fv1,
+              const orb_frame_view_t* V2, const uint8_t* flag2, orb_feature_vector_t fv2, const float* F12,
+              float nnratio, int check_ori, int32_t* out, int* n_out, int device) {
+    int st;
+    if ((st = check_view(V1, "query frame")) || (st = check_view(V2, "target frame"))) return st;
+    if (!out || !n_out || !flag1 || (mode != M_BOW_KFF && !flag2) || (mode == M_TRIANG && !F12))
+        return fail(ORB_EINVAL, "bad arguments");
+    if (bad_fv(fv1, V1->n) || bad_fv(fv2, V2->n)) return fail(ORB_EINVAL, "malformed FeatureVector");
+    const bool byTarget = mode == M_BOW_KFF;
+    const int outN = byTarget ? V2->n : V1->n;
+    *n_out = 0;
+    if (V1->n == 0 || V2->n == 0 || fv1.n_nodes == 0 || fv2.n_nodes == 0) {
+        for (int i = 0; i < outN; ++i) out[i] = -1;
+        return ORB_OK;
+    }
+    const int qn = fv1.offsets[fv1.n_nodes];
+    Call C{device};
+    if ((st = C.begin())) return st;
+    std::lock_guard<std::mutex> lk(C.ctx->mu);
+    DeviceGuard dg(device);
+    Arena& A = C.A;
+    const size_t o1k = A.stage(V1->kps, (size_t)V1->n * sizeof(orb_keypoint_t));
+    const size_t o1d = A.stage(V1->desc, (size_t)V1->n * 32);
+    const size_t o1f = A.stage(flag1, (size_t)V1->n);
+    const size_t o2k = A.stage(V2->kps, (size_t)V2->n * sizeof(orb_keypoint_t));
+    const size_t o2d = A.stage(V2->desc, (size_t)V2->n * 32);
+    const size_t o2f = flag2 ? A.stage(flag2, (size_t)V2->n) : 0;
+    const size_t on1 = A.stage(fv1.nodes, (size_t)fv1.n_nodes * 4);
+    const size_t oo1 = A.stage(fv1.offsets, (size_t)(fv1.n_nodes + 1) * 4);
+    const size_t of1 = A.stage(fv1.features, (size_t)qn * 4);
+    const size_t on2 = A.stage(fv2.nodes, (size_t)fv2.n_nodes * 4);
+    const size_t oo2 = A.stage(fv2.offsets, (size_t)(fv2.n_nodes + 1) * 4);
+    const size_t of2 = A.stage(fv2.features, (size_t)fv2.offsets[fv2.n_nodes] * 4);
+    const JobOffs jo = plan_job(A, qn, outN);
+    if ((st = C.commit())) return st;
+    Job J = base_job(mode);
+    J.T.kps = C.at<orb_keypoint_t>(o2k);
+    J.T.desc = C.at<uint32_t>(o2d);
+    J.T.n = V2->n;
+    J.T.nlevels = V2->nlevels;
+    std::memcpy(J.T.sigma2, V2->level_sigma2, sizeof(J.T.sigma2));
+    std::memcpy(J.T.sf, V2->scale_factors, sizeof(J.T.sf));
+    J.T.items = C.at<int>(of2);
+    J.qkps = C.at<orb_keypoint_t>(o1k);
+    J.qdesc = C.at<uint32_t>(o1d);
+    J.qflag = C.at<uint8_t>(o1f);
+    J.tflag = flag2 ? C.at<uint8_t>(o2f) : nullptr;
+    J.fv1Nodes = C.at<uint32_t>(on1);
+    J.fv1Off = C.at<int>(oo1);
+    J.fv1Feat = C.at<int>(of1);
+    J.fv1N = fv1.n_nodes;
+    J.fv2Nodes = C.at<uint32_t>(on2);
+    J.fv2Off = C.at<int>(oo2);
+    J.fv2N = fv2.n_nodes;
+    J.nnratio = nnratio;
+    J.checkOri = check_ori;
+    if (F12) std::memcpy(J.F12, F12, sizeof(J.F12));
+    J.outByTarget = byTarget;
+    bind_job(C, J, jo, qn, outN);
+    if ((st = run_job(C, J))) return st;
+    int nm = 0;
+    if ((st = C.download(out, jo.out, (size_t)outN * 4)) || (st = C.download(&nm, jo.nOut, 4)) || (st = C.sync()))
+        return st;
+    *n_out = nm;
+    return ORB_OK;
+}
+
+// Shared driver of the grid matchers: target view + queries -> one job.
+struct GridQueries {
+    int qn = 0;
+    const uint8_t* flag = nullptr;
+    const uint8_t* desc = nullptr;        // qn x 32 (or the query frame's descriptors)
+    const orb_keypoint_t* kps = nullptr;  // query frame keypoints (qn)
+    const float* pos = nullptr;
+    const float* normal = nullptr;
+    const float* dmin = nullptr;
+    const float* dmax = nullptr;
+    const float* u = nullptr;
+    const float* v = nullptr;
+    const int32_t* level = nullptr;
+    int levelStride = 1;
+    const float* vcos = nullptr;
+};
+
+int grid_match(Job J, const orb_frame_view_t* T, const uint8_t* taken, const GridQueries& Q, int32_t* out,
+               int* n_out, int device, int outByTarget) {
+    int st;
+    if ((st = check_view(T, "target frame"))) return st;
+    if (!out || !n_out || Q.qn < 0) return fail(ORB_EINVAL, "bad arguments");
+    const int outN = outByTarget ? T->n : Q.qn;
+    *n_out = 0;
+    if (T->n == 0 || Q.qn == 0) {
+        for (int i = 0; i < outN; ++i) out[i] = -1;
+        return ORB_OK;
+    }
+    Call C{device};
+    if ((st = C.begin())) return st;
+    std::lock_guard<std::mutex> lk(C.ctx->mu);
+    DeviceGuard dg(device);
+    Arena& A = C.A;
+    const ViewOffs vo = plan_view(A, T, true);
+    const size_t oTaken = taken ? A.stage(taken, (size_t)T->n) : 0;
+    const size_t oFlag = Q.flag ? A.stage(Q.flag, (size_t)Q.qn) : 0;
+    const size_t oDesc = Q.desc ? A.stage(Q.desc, (size_t)Q.qn * 32) : 0;
+    const size_t oKps = Q.kps ? A.stage(Q.kps, (size_t)Q.qn * sizeof(orb_keypoint_t)) : 0;
+    const size_t oPos = Q.pos ? A.stage(Q.pos, (size_t)Q.qn * 12) : 0;
+    const size_t oNrm = Q.normal ? A.stage(Q.normal, (size_t)Q.qn * 12) : 0;
+    const size_t oDmin = Q.dmin ? A.stage(Q.dmin, (size_t)Q.qn * 4) : 0;
+    const size_t oDmax = Q.dmax ? A.stage(Q.dmax, (size_t)Q.qn * 4) : 0;
+    const size_t oU = Q.u ? A.stage(Q.u, (size_t)Q.qn * 4) : 0;
+    const size_t oV = Q.v ? A.stage(Q.v, (size_t)Q.qn * 4) : 0;
+    const size_t oL = Q.level ? A.stage(Q.level, (size_t)Q.qn * 4 * Q.levelStride) : 0;
+    const size_t oC = Q.vcos ? A.stage(Q.vcos, (size_t)Q.qn * 4) : 0;
+    const JobOffs jo = plan_job(A, Q.qn, outN);
+    if ((st = C.commit())) return st;
+    J.T = make_dview(C, T, vo, true);
+    if ((st = launch_grid(C, J.T))) return st;
+    J.taken0 = taken ? C.at<uint8_t>(oTaken) : nullptr;
+    J.qflag = Q.flag ? C.at<uint8_t>(oFlag) : nullptr;
+    J.qdesc = Q.desc ? C.at<uint32_t>(oDesc) : nullptr;
+    J.qkps = Q.kps ? C.at<orb_keypoint_t>(oKps) : nullptr;
+    J.qpos = Q.pos ? C.at<float>(oPos) : nullptr;
+    J.qnormal = Q.normal ? C.at<float>(oNrm) : nullptr;
+    J.qdmin = Q.dmin ? C.at<float>(oDmin) : nullptr;
+    J.qdmax = Q.dmax ? C.at<float>(oDmax) : nullptr;
+    J.qu = Q.u ? C.at<float>(oU) : nullptr;
+    J.qv = Q.v ? C.at<float>(oV) : nullptr;
+    J.qlevel = Q.level ? C.at<int>(oL) : nullptr;
+    J.qvcos = Q.vcos ? C.at<float>(oC) : nullptr;
+    J.outByTarget = outByTarget;
+    bind_job(C, J, jo, Q.qn, outN);
+    if ((st = run_job(C, J))) return st;
+    int nm = 0;
+    if ((st = C.download(out, jo.out, (size_t)outN * 4)) || (st = C.download(&nm, jo.nOut, 4)) || (st = C.sync()))
+        return st;
+    *n_out = nm;
+    return ORB_OK;
+}
+
+bool finite_pose(const orb_frame_view_t* v) {
+    for (int i = 0; i < 9; ++i)
+        if (!std::isfinite(v->Rcw[i])) return false;
+    for (int i = 0; i < 3; ++i)
+        if (!std::isfinite(v->tcw[i]) || !std::isfinite(v->Ow[i])) return false;
+    return true;
+}
+
+}  // namespace
+
+// =========================================================================================
+// C ABI
+// =========================================================================================
+extern "C" {
+
+int orb_features_in_area(const orb_frame_view_t* view, int keyframe, int q, const float* x, const float* y,
+                         const float* r, const int32_t* min_level, const int32_t* max_level, int32_t* out_offsets,
+                         int32_t* out_indices, int capacity, int device) {
+    int st;
+    if ((st = check_view(view, "frame"))) return st;
+    if (q < 0 || !out_offsets || (q > 0 && (!x || !y || !r)) || capacity < 0 || (capacity > 0 && !out_indices))
+        return fail(ORB_EINVAL, "bad arguments");
+    if (!keyframe && ((min_level == nullptr) != (max_level == nullptr)))
+        return fail(ORB_EINVAL, "min_level and max_level go together");
+    out_offsets[0] = 0;
+    if (q == 0) return ORB_OK;
+    if (view->n == 0) {
+        for (int i = 0; i <= q; ++i) out_offsets[i] = 0;
+        return ORB_OK;
+    }
+    Call C{device};
+    if ((st = C.begin())) return st;
+    std::lock_guard<std::mutex> lk(C.ctx->mu);
+    DeviceGuard dg(device);
+    Arena& A = C.A;
+    const ViewOffs vo = plan_view(A, view, true);
+    const size_t ox = A.stage(x, (size_t)q * 4), oy = A.stage(y, (size_t)q * 4), orr = A.stage(r, (size_t)q * 4);
+    std::vector<int32_t> lv;
+    size_t ol = 0;
+    if (!keyframe && min_level) {
+        lv.resize((size_t)2 * q);
+        for (int i = 0; i < q; ++i) {
+            lv[2 * i] = min_level[i];
+            lv[2 * i + 1] = max_level[i];
+        }
+        ol = A.stage(lv.data(), lv.size() * 4);
+    }
+    const JobOffs jo = plan_job(A, q, 1);
+    const size_t oOff = A.take((size_t)(q + 1) * 4);
+    const size_t oOut = A.take((size_t)std::max(capacity, 1) * 4);
+    if ((st = C.commit())) return st;
+    Job J = base_job(keyframe ? M_AREA_KF : M_AREA_F);
+    J.T = make_dview(C, view, vo, true);
+    if ((st = launch_grid(C, J.T))) return st;
+    J.qu = C.at<float>(ox);
+    J.qv = C.at<float>(oy);
+    J.qvcos = C.at<float>(orr);
+    J.qlevel = ol ? C.at<int>(ol) : nullptr;
+    bind_job(C, J, jo, q, 1);
+    J.areaOff = C.at<int>(oOff);
+    J.areaOut = C.at<int>(oOut);
+    hipStream_t s = C.ctx->stream;
+    hipLaunchKernelGGL(k_query_prep, dim3((q + 255) / 256), dim3(256), 0, s, J);
+    hipLaunchKernelGGL(k_query_scan, dim3((q + 3) / 4), dim3(256), 0, s, J);
+    HIPCHK(hipGetLastError());
+    std::vector<int> cnt(q);
+    if ((st = C.download(cnt.data(), jo.cnt, (size_t)q * 4)) || (st = C.sync())) return st;
+    long long tot = 0;
+    for (int i = 0; i < q; ++i) {
+        out_offsets[i] = (int32_t)std::min<long long>(tot, INT_MAX);
+        tot += cnt[i];
+    }
+    out_offsets[q] = (int32_t)std::min<long long>(tot, INT_MAX);
+    if (tot > capacity) return fail(ORB_ERANGE, "candidate capacity too small");
+    if (tot == 0) return ORB_OK;
+    HIPCHK(hipMemcpyAsync(J.areaOff, out_offsets, (size_t)(q + 1) * 4, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_area_fill, dim3((q + 3) / 4), dim3(256), 0, s, J);
+    HIPCHK(hipGetLastError());
+    if ((st = C.download(out_indices, oOut, (size_t)tot * 4)) || (st = C.sync())) return st;
+    return ORB_OK;
+}
+
+int orb_frame_is_in_frustum(const orb_frame_view_t* F, orb_map_points_t mps, float viewing_cos_limit,
+                            uint8_t* in_view, float* proj_x, float* proj_y, int32_t* level, float* view_cos,
+                            int device);
+
+int orb_search_by_bow_kf_f(const orb_frame_view_t* KF, const uint8_t* kf_usable, orb_feature_vector_t kf_fv,
+                           const orb_frame_view_t* F, orb_feature_vector_t f_fv, float nnratio, int check_ori,
+                           int32_t* f_match, int* n_matches, int device) {
+    return bow_match(M_BOW_KFF, KF, kf_usable, kf_fv, F, nullptr, f_fv, nullptr, nnratio, check_ori, f_match,
+                     n_matches, device);
+}
+
+int orb_search_by_bow_kf_kf(const orb_frame_view_t* KF1, const uint8_t* usable1, orb_feature_vector_t fv1,
+                            const orb_frame_view_t* KF2, const uint8_t* usable2, orb_feature_vector_t fv2,
+                            float nnratio, int check_ori, int32_t* match12, int* n_matches, int device) {
+    return bow_match(M_BOW_KFKF, KF1, usable1, fv1, KF2, usable2, fv2, nullptr, nnratio, check_ori, match12,
+                     n_matches, device);
+}
+
+int orb_search_for_triangulation(const orb_frame_view_t* KF1, const uint8_t* has_mp1, orb_feature_vector_t fv1,
+                                 const orb_frame_view_t* KF2, const uint8_t* has_mp2, orb_feature_vector_t fv2,
+                                 const float* F12, float nnratio, int check_ori, int32_t* match12, int* n_matches,
+                                 int device) {
+    return bow_match(M_TRIANG, KF1, has_mp1, fv1, KF2, has_mp2, fv2, F12, nnratio, check_ori, match12, n_matches,
+                     device);
+}
+
+int orb_window_search(const orb_frame_view_t* F1, const uint8_t* usable1, const orb_frame_view_t* F2, int window,
+                      int min_scale_level, int max_scale_level, float nnratio, int check_ori, int32_t* match21,
+                      int* n_matches, int device) {
+    int st;
+    if ((st = check_view(F1, "F1"))) return st;
+    if (F1->n && !usable1) return fail(ORB_EINVAL, "usable1 is NULL");
+    Job J = base_job(M_WINDOW);
+    J.window = window;
+    J.minLevel = min_scale_level;
+    J.maxLevel = max_scale_level;
+    J.nnratio = nnratio;
+    J.checkOri = check_ori;
+    GridQueries Q;
+    Q.qn = F1->n;
+    Q.flag = usable1;
+    Q.desc = F1->desc;
+    Q.kps = F1->kps;
+    return grid_match(J, F2, nullptr, Q, match21, n_matches, device, 1);
+}
+
+int orb_search_by_projection_local(const orb_frame_view_t* F, const uint8_t* f_taken, int n_mp, const uint8_t* usable,
+                                   const float* proj_x, const float* proj_y, const int32_t* level,
+                                   const float* view_cos, const uint8_t* mp_desc, float th, float nnratio,
+                                   int32_t* f_match, int* n_matches, int device) {
+    int st;
+    if ((st = check_view(F, "F"))) return st;
+    if (n_mp < 0 || (n_mp > 0 && (!usable || !proj_x || !proj_y || !level || !view_cos || !mp_desc)))
+        return fail(ORB_EINVAL, "bad MapPoint arrays");
+    for (int i = 0; i < n_mp; ++i)
+        if (usable[i] && (level[i] < 0 || level[i] >= F->nlevels)) return fail(ORB_EINVAL, "predicted level out of range");
+    Job J = base_job(M_LOCAL);
+    J.th = th;
+    J.nnratio = nnratio;
+    GridQueries Q;
+    Q.qn = n_mp;
+    Q.flag = usable;
+    Q.desc = mp_desc;
+    Q.u = proj_x;
+    Q.v = proj_y;
+    Q.level = level;
+    Q.vcos = view_cos;
+    return grid_match(J, F, f_taken, Q, f_match, n_matches, device, 1);
+}
+
+int orb_search_by_projection_f2f(const orb_frame_view_t* F1, orb_map_points_t mp1, const uint8_t* usable1,
+                                 const orb_frame_view_t* F2, const uint8_t* f2_taken, int window, float nnratio,
+                                 int32_t* match2, int* n_matches, int device) {
+    int st;
+    if ((st = check_view(F1, "F1"))) return st;
+    if (F1->n && (!usable1 || !mp1.pos || mp1.n < F1->n)) return fail(ORB_EINVAL, "bad F1 MapPoint arrays");
+    if (!finite_pose(F2)) return fail(ORB_EINVAL, "F2 pose not finite");
+    Job J = base_job(M_F2F);
+    J.window = window;
+    J.nnratio = nnratio;
+    GridQueries Q;
+    Q.qn = F1->n;
+    Q.flag = usable1;
+    Q.desc = F1->desc;
+    Q.kps = F1->kps;
+    Q.pos = mp1.pos;
+    return grid_match(J, F2, f2_taken, Q, match2, n_matches, device, 1);
+}
+
+int orb_search_by_projection_motion(const orb_frame_view_t* Cur, const uint8_t* cur_taken, const orb_frame_view_t* Last,
+                                    orb_map_points_t mp, const uint8_t* usable, float th, int check_ori,
+                                    int32_t* cur_match, int* n_matches, int device) {
+    int st;
+    if ((st = check_view(Last, "LastFrame"))) return st;
+    if (Last->n && (!usable || !mp.pos || mp.n < Last->n)) return fail(ORB_EINVAL, "bad LastFrame MapPoint arrays");
+    if (Cur && Last->nlevels > Cur->nlevels) return fail(ORB_EINVAL, "LastFrame has more levels than CurrentFrame");
+    Job J = base_job(M_MOTION);
+    J.th = th;
+    J.checkOri = check_ori;
+    GridQueries Q;
+    Q.qn = Last->n;
+    Q.flag = usable;
+    Q.desc = Last->desc;
+    Q.kps = Last->kps;
+    Q.pos = mp.pos;
+    return grid_match(J, Cur, cur_taken, Q, cur_match, n_matches, device, 1);
+}
+
+int orb_search_by_projection_reloc(const orb_frame_view_t* Cur, const uint8_t* cur_taken, const orb_frame_view_t* KF,
+                                   orb_map_points_t mp, const uint8_t* usable, float th, int orb_dist,
+                                   int check_ori, int32_t* cur_match, int* n_matches, int device) {
+    int st;
+    if ((st = check_view(KF, "KF"))) return st;
+    if (KF->n && (!usable || !mp.pos || !mp.dmin || !mp.desc || mp.n < KF->n))
+        return fail(ORB_EINVAL, "bad KF MapPoint arrays");
+    Job J = base_job(M_RELOC);
+    J.th = th;
+    J.thDist = orb_dist;
+    J.checkOri = check_ori;
+    GridQueries Q;
+    Q.qn = KF->n;
+    Q.flag = usable;
+    Q.desc = mp.desc;
+    Q.kps = KF->kps;
+    Q.pos = mp.pos;
+    Q.dmin = mp.dmin;
+    return grid_match(J, Cur, cur_taken, Q, cur_match, n_matches, device, 1);
+}
+
+int orb_search_by_projection_sim3(const orb_frame_view_t* KF, const uint8_t* kf_taken, orb_map_points_t pts,
+                                  const uint8_t* usable, int th, int32_t* kf_match, int* n_matches, int device) {
+    if (pts.n < 0 || (pts.n > 0 && (!usable || !pts.pos || !pts.normal || !pts.dmin || !pts.dmax || !pts.desc)))
+        return fail(ORB_EINVAL, "bad point arrays");
+    Job J = base_job(M_SIM3P);
+    J.th = (float)th;
+    J.thDist = TH_LOW;
+    GridQueries Q;
+    Q.qn = pts.n;
+    Q.flag = usable;
+    Q.desc = pts.desc;
+    Q.pos = pts.pos;
+    Q.normal = pts.normal;
+    Q.dmin = pts.dmin;
+    Q.dmax = pts.dmax;
+    return grid_match(J, KF, kf_taken, Q, kf_match, n_matches, device, 1);
+}
+
+int orb_fuse(const orb_frame_view_t* KF, orb_map_points_t pts, const uint8_t* usable, float th, int scw,
+             int32_t* best_idx, int* n_fused, int device) {
+    if (pts.n < 0 || (pts.n > 0 && (!usable || !pts.pos || !pts.normal || !pts.dmin || !pts.dmax || !pts.desc)))
+        return fail(ORB_EINVAL, "bad point arrays");
+    Job J = base_job(scw ? M_FUSE_SCW : M_FUSE);
+    J.th = th;
+    J.thDist = TH_LOW;
+    GridQueries Q;
+    Q.qn = pts.n;
+    Q.flag = usable;
+    Q.desc = pts.desc;
+    Q.pos = pts.pos;
+    Q.normal = pts.normal;
+    Q.dmin = pts.dmin;
+    Q.dmax = pts.dmax;
+    return grid_match(J, KF, nullptr, Q, best_idx, n_fused, device, 0);
+}
+
+int orb_search_by_sim3(const orb_frame_view_t* KF1, orb_map_points_t mp1, const uint8_t* usable1,
+                       const orb_frame_view_t* KF2, orb_map_points_t mp2, const uint8_t* usable2, const float* sR12,
+                       const float* t12, const float* sR21, const float* t21, float th, int32_t* match12,
+                       int* n_found, int device) {
+    int st;
+    if ((st = check_view(KF1, "KF1")) || (st = check_view(KF2, "KF2"))) return st;
+    if (!sR12 || !t12 || !sR21 || !t21 || !match12 || !n_found) return fail(ORB_EINVAL, "bad arguments");
+    if ((KF1->n && (!usable1 || !mp1.pos || !mp1.dmin || !mp1.dmax || !mp1.desc || mp1.n < KF1->n)) ||
+        (KF2->n && (!usable2 || !mp2.pos || !mp2.dmin || !mp2.dmax || !mp2.desc || mp2.n < KF2->n)))
+        return fail(ORB_EINVAL, "bad MapPoint arrays");
+    // direction 1: KF1's points into KF2 -> vnMatch1 (n1); direction 2: KF2's into KF1 -> vnMatch2 (n2)
+    std::vector<int32_t> m1(KF1->n), m2(KF2->n);
+    int n1 = 0, n2 = 0;
+    for (int dir = 0; dir < 2; ++dir) {
+        const orb_frame_view_t* src = dir ? KF2 : KF1;
+        const orb_frame_view_t* dst = dir ? KF1 : KF2;
+        const orb_map_points_t& mp = dir ? mp2 : mp1;
+        Job J = base_job(M_SIM3);
+        J.th = th;
+        J.thDist = TH_HIGH;
+        std::memcpy(J.SRw, src->Rcw, sizeof(J.SRw));
+        std::memcpy(J.Stw, src->tcw, sizeof(J.Stw));
+        std::memcpy(J.SR, dir ? sR12 : sR21, sizeof(J.SR));
+        std::memcpy(J.St, dir ? t12 : t21, sizeof(J.St));
+        J.qfx = KF1->fx;  // pKF1's calibration for both directions (ORBmatcher.cc:1270-1273)
+        J.qfy = KF1->fy;
+        J.qcx = KF1->cx;
+        J.qcy = KF1->cy;
+        GridQueries Q;
+        Q.qn = src->n;
+        Q.flag = dir ? usable2 : usable1;
+        Q.desc = mp.desc;
+        Q.pos = mp.pos;
+        Q.dmin = mp.dmin;
+        Q.dmax = mp.dmax;
+        if ((st = grid_match(J, dst, nullptr, Q, dir ? m2.data() : m1.data(), dir ? &n2 : &n1, device, 0))) return st;
+    }
+    // agreement on the device of the call (tiny; keeps the selection off the host)
+    Call C{device};
+    if ((st = C.begin())) return st;
+    std::lock_guard<std::mutex> lk(C.ctx->mu);
+    DeviceGuard dg(device);
+    const size_t o1 = C.A.stage(m1.data(), m1.size() * 4), o2 = C.A.stage(m2.data(), m2.size() * 4);
+    const size_t oo = C.A.take(std::max<size_t>(m1.size(), 1) * 4), on = C.A.take(16);
+    if ((st = C.commit())) return st;
+    hipLaunchKernelGGL(k_sim3_agree, dim3(1), dim3(256), 0, C.ctx->stream, C.at<int>(o1), KF1->n, C.at<int>(o2),
+                       C.at<int>(oo), C.at<int>(on));
+    HIPCHK(hipGetLastError());
+    int nf = 0;
+    if ((st = C.download(match12, oo, m1.size() * 4)) || (st = C.download(&nf, on, 4)) || (st = C.sync())) return st;
+    *n_found = nf;
+    return ORB_OK;
+}
+
+}  // extern "C"
+
+// ---- Frame::isInFrustum (Frame.cc:137-198), one thread per MapPoint ----------------------
+namespace {
+__global__ void __launch_bounds__(256) k_is_in_frustum(DView T, const float* __restrict__ pos,
+                                                       const float* __restrict__ normal, const float* __restrict__ dmin,
+                                                       const float* __restrict__ dmax, int n, float limit,
+                                                       uint8_t* __restrict__ inView, float* __restrict__ px,
+                                                       float* __restrict__ py, int* __restrict__ lv,
+                                                       float* __restrict__ vc) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    uint8_t ok = 0;
+    float u = 0.f, v = 0.f, viewCos = 0.f;
+    int pred = -1;
+    do {
+        const float* P = pos + 3 * i;
+        float Pc[3];
+        gemm3_add(T.R, P, T.t, Pc);
+        const float PcX = Pc[0], PcY = Pc[1], PcZ = Pc[2];
+        if (PcZ < 0.0f) break;
+        const float invz = (float)(1.0 / (double)PcZ);
+        const float uu = __builtin_fmaf(T.fx * PcX, invz, T.cx);
+        const float vv = __builtin_fmaf(T.fy * PcY, invz, T.cy);
+        if (uu < (float)T.minX || uu > (float)T.maxX) break;
+        if (vv < (float)T.minY || vv > (float)T.maxY) break;
+        const float maxDistance = dmax[i], minDistance = dmin[i];
+        float PO[3] = {P[0] - T.Ow[0], P[1] - T.Ow[1], P[2] - T.Ow[2]};
+        const float dist = (float)norm3(PO);
+        if (dist < minDistance || dist > maxDistance) break;
+        const float vcos = (float)(dot3(PO, normal + 3 * i) / (double)dist);
+        if (vcos < limit) break;
+        const float ratio = dist / minDistance;
+        int nPred = 0;
+        while (nPred < T.nlevels && T.sf[nPred] < ratio) ++nPred;
+        if (nPred >= T.nlevels) nPred = T.nlevels - 1;
+        ok = 1;
+        u = uu;
+        v = vv;
+        viewCos = vcos;
+        pred = nPred;
+    } while (0);
+    inView[i] = ok;
+    px[i] = u;
+    py[i] = v;
+    lv[i] = pred;
+    vc[i] = viewCos;
+}
+}  // namespace
+
+extern "C" int orb_frame_is_in_frustum(const orb_frame_view_t* F, orb_map_points_t mps, float viewing_cos_limit,
+                                       uint8_t* in_view, float* proj_x, float* proj_y, int32_t* level,
+                                       float* view_cos, int device) {
+    if (!F || F->nlevels < 1 || F->nlevels > ORB_MAX_VIEW_LEVELS || mps.n < 0 ||
+        (mps.n > 0 && (!mps.pos || !mps.normal || !mps.dmin || !mps.dmax || !in_view || !proj_x || !proj_y || !level ||
+                       !view_cos)))
+        return fail(ORB_EINVAL, "bad arguments");
+    if (mps.n == 0) return ORB_OK;
+    int st;
+    Call C{device};
+    if ((st = C.begin())) return st;
+    std::lock_guard<std::mutex> lk(C.ctx->mu);
+    DeviceGuard dg(device);
+    Arena& A = C.A;
+    const size_t n = (size_t)mps.n;
+    const size_t op = A.stage(mps.pos, n * 12), onr = A.stage(mps.normal, n * 12), omn = A.stage(mps.dmin, n * 4),
+                 omx = A.stage(mps.dmax, n * 4);
+    const size_t oi = A.take(n), ox = A.take(n * 4), oy = A.take(n * 4), ol = A.take(n * 4), oc = A.take(n * 4);
+    if ((st = C.commit())) return st;
+    orb_frame_view_t Fv = *F;
+    Fv.n = 0;
+    Fv.kps = nullptr;
+    Fv.desc = nullptr;
+    ViewOffs vo{};
+    DView d = make_dview(C, &Fv, vo, false);
+    hipLaunchKernelGGL(k_is_in_frustum, dim3((mps.n + 255) / 256), dim3(256), 0, C.ctx->stream, d, C.at<float>(op),
+                       C.at<float>(onr), C.at<float>(omn), C.at<float>(omx), mps.n, viewing_cos_limit,
+                       C.at<uint8_t>(oi), C.at<float>(ox), C.at<float>(oy), C.at<int>(ol), C.at<float>(oc));
+    HIPCHK(hipGetLastError());
+    if ((st = C.download(in_view, oi, n)) || (st = C.download(proj_x, ox, n * 4)) ||
+        (st = C.download(proj_y, oy, n * 4)) || (st = C.download(level, ol, n * 4)) ||
+        (st = C.download(view_cos, oc, n * 4)) || (st = C.sync()))
+        return st;
+    return ORB_OK;
+}

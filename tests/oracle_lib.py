@@ -137,3 +137,176 @@ def search_for_initialization(k1, d1, k2, d2, width, height, prev, nnratio=0.9, 
                                             _p(m12), ctypes.byref(n))
     assert st == 0
     return n.value, m12
+
+
+# ---- the rest of the ORBmatcher family (oracle/orb_oracle_match.cpp) -----------------------
+def _bind_family(L):
+    from orbslam_jpminipc_amd._native import FeatureVectorCSR, FrameView, MapPoints
+
+    vp, i, f = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    pv, pi = ctypes.POINTER(FrameView), ctypes.POINTER(ctypes.c_int)
+    sig = {
+        "oracle_features_in_area_view": [pv, i, f, f, f, i, i, vp, i],
+        "oracle_frame_is_in_frustum": [pv, MapPoints, f, vp, vp, vp, vp, vp],
+        "oracle_search_by_projection_local": [pv, vp, i, vp, vp, vp, vp, vp, vp, f, f, vp, pi],
+        "oracle_window_search": [pv, vp, pv, i, i, i, f, i, vp, pi],
+        "oracle_search_by_projection_f2f": [pv, MapPoints, vp, pv, vp, i, f, vp, pi],
+        "oracle_search_by_projection_motion": [pv, vp, pv, MapPoints, vp, f, i, vp, pi],
+        "oracle_search_by_projection_reloc": [pv, vp, pv, MapPoints, vp, f, i, i, vp, pi],
+        "oracle_search_by_projection_sim3": [pv, vp, MapPoints, vp, i, vp, pi],
+        "oracle_fuse": [pv, MapPoints, vp, f, i, vp, pi],
+        "oracle_search_by_sim3": [pv, MapPoints, vp, pv, MapPoints, vp, vp, vp, vp, vp, f, vp, pi],
+        "oracle_search_for_triangulation": [pv, vp, FeatureVectorCSR, pv, vp, FeatureVectorCSR, vp, f, i, vp, pi],
+    }
+    for k, a in sig.items():
+        getattr(L, k).argtypes = a
+        getattr(L, k).restype = i
+
+
+class OracleMatcher:
+    """CPU restatement with the same method surface as orbslam_jpminipc_amd.ORBmatcher's
+    family methods (views.View / MapPointSet / FeatureVector in, (n, index array) out)."""
+
+    def __init__(self, nnratio=0.6, checkOri=True):
+        self.L = lib()
+        if not getattr(self.L, "_family_bound", False):
+            _bind_family(self.L)
+            self.L._family_bound = True
+        self.mfNNratio = float(nnratio)
+        self.mbCheckOrientation = bool(checkOri)
+
+    @staticmethod
+    def _u8(a, n, default=1):
+        if a is None:
+            return np.full(n, default, np.uint8)
+        return np.ascontiguousarray(np.asarray(a, np.uint8).reshape(-1))
+
+    def SearchByBoW_KF_F(self, KF, kf_usable, kf_fv, F, f_fv):
+        out = np.full(F.n, -1, np.int32)
+        n = ctypes.c_int()
+        u = self._u8(kf_usable, KF.n)
+        st = self.L.oracle_search_by_bow_kf_f(_p(KF.kps), _p(KF.desc), KF.n, _p(u), _p(kf_fv.nodes),
+                                              _p(kf_fv.offsets), _p(kf_fv.features), len(kf_fv.nodes), _p(F.kps),
+                                              _p(F.desc), F.n, _p(f_fv.nodes), _p(f_fv.offsets), _p(f_fv.features),
+                                              len(f_fv.nodes), self.mfNNratio, int(self.mbCheckOrientation),
+                                              _p(out), ctypes.byref(n))
+        assert st == 0
+        return n.value, out
+
+    def SearchByBoW_KF_KF(self, KF1, usable1, fv1, KF2, usable2, fv2):
+        out = np.full(KF1.n, -1, np.int32)
+        n = ctypes.c_int()
+        u1, u2 = self._u8(usable1, KF1.n), self._u8(usable2, KF2.n)
+        st = self.L.oracle_search_by_bow_kf_kf(_p(KF1.kps), _p(KF1.desc), KF1.n, _p(u1), _p(fv1.nodes),
+                                               _p(fv1.offsets), _p(fv1.features), len(fv1.nodes), _p(KF2.kps),
+                                               _p(KF2.desc), KF2.n, _p(u2), _p(fv2.nodes), _p(fv2.offsets),
+                                               _p(fv2.features), len(fv2.nodes), self.mfNNratio,
+                                               int(self.mbCheckOrientation), _p(out), ctypes.byref(n))
+        assert st == 0
+        return n.value, out
+
+    def SearchForTriangulation(self, KF1, has_mp1, fv1, KF2, has_mp2, fv2, F12):
+        out = np.full(KF1.n, -1, np.int32)
+        n = ctypes.c_int()
+        h1, h2 = self._u8(has_mp1, KF1.n, 0), self._u8(has_mp2, KF2.n, 0)
+        F = np.ascontiguousarray(np.asarray(F12, np.float32).reshape(9))
+        st = self.L.oracle_search_for_triangulation(KF1.ref(), _p(h1), fv1.struct(), KF2.ref(), _p(h2),
+                                                    fv2.struct(), _p(F), self.mfNNratio,
+                                                    int(self.mbCheckOrientation), _p(out), ctypes.byref(n))
+        assert st == 0
+        return n.value, out
+
+    def WindowSearch(self, F1, usable1, F2, windowSize, minScaleLevel=0, maxScaleLevel=2**31 - 1):
+        out = np.full(F2.n, -1, np.int32)
+        n = ctypes.c_int()
+        u = self._u8(usable1, F1.n)
+        st = self.L.oracle_window_search(F1.ref(), _p(u), F2.ref(), int(windowSize), int(minScaleLevel),
+                                         int(maxScaleLevel), self.mfNNratio, int(self.mbCheckOrientation), _p(out),
+                                         ctypes.byref(n))
+        assert st == 0
+        return n.value, out
+
+    def SearchByProjection_Local(self, F, f_taken, usable, proj_x, proj_y, level, view_cos, mp_desc, th=1.0):
+        m = len(proj_x)
+        out = np.full(F.n, -1, np.int32)
+        n = ctypes.c_int()
+        tk, u = self._u8(f_taken, F.n, 0), self._u8(usable, m)
+        a = [np.ascontiguousarray(np.asarray(x, t)) for x, t in
+             ((proj_x, np.float32), (proj_y, np.float32), (level, np.int32), (view_cos, np.float32))]
+        d = np.ascontiguousarray(np.asarray(mp_desc, np.uint8).reshape(-1, 32))
+        st = self.L.oracle_search_by_projection_local(F.ref(), _p(tk), m, _p(u), *map(_p, a), _p(d), float(th),
+                                                      self.mfNNratio, _p(out), ctypes.byref(n))
+        assert st == 0
+        return n.value, out
+
+    def isInFrustum(self, F, mps, viewingCosLimit=0.5):
+        m = mps.n
+        iv = np.zeros(m, np.uint8)
+        px, py, vc = (np.zeros(m, np.float32) for _ in range(3))
+        lv = np.zeros(m, np.int32)
+        st = self.L.oracle_frame_is_in_frustum(F.ref(), mps.struct(), float(viewingCosLimit), _p(iv), _p(px), _p(py),
+                                               _p(lv), _p(vc))
+        assert st == 0
+        return iv, px, py, lv, vc
+
+    def SearchByProjection_F2F(self, F1, mp1, usable1, F2, f2_taken, windowSize):
+        out = np.full(F2.n, -1, np.int32)
+        n = ctypes.c_int()
+        u, tk = self._u8(usable1, F1.n), self._u8(f2_taken, F2.n, 0)
+        st = self.L.oracle_search_by_projection_f2f(F1.ref(), mp1.struct(), _p(u), F2.ref(), _p(tk),
+                                                    int(windowSize), self.mfNNratio, _p(out), ctypes.byref(n))
+        assert st == 0
+        return n.value, out
+
+    def SearchByProjection_Motion(self, Cur, cur_taken, Last, mp, usable, th):
+        out = np.full(Cur.n, -1, np.int32)
+        n = ctypes.c_int()
+        tk, u = self._u8(cur_taken, Cur.n, 0), self._u8(usable, Last.n)
+        st = self.L.oracle_search_by_projection_motion(Cur.ref(), _p(tk), Last.ref(), mp.struct(), _p(u), float(th),
+                                                       int(self.mbCheckOrientation), _p(out), ctypes.byref(n))
+        assert st == 0
+        return n.value, out
+
+    def SearchByProjection_Reloc(self, Cur, cur_taken, KF, mp, usable, th, ORBdist):
+        out = np.full(Cur.n, -1, np.int32)
+        n = ctypes.c_int()
+        tk, u = self._u8(cur_taken, Cur.n, 0), self._u8(usable, KF.n)
+        st = self.L.oracle_search_by_projection_reloc(Cur.ref(), _p(tk), KF.ref(), mp.struct(), _p(u), float(th),
+                                                      int(ORBdist), int(self.mbCheckOrientation), _p(out),
+                                                      ctypes.byref(n))
+        assert st == 0
+        return n.value, out
+
+    def SearchByProjection_Sim3(self, KF, kf_taken, pts, usable, th):
+        out = np.full(KF.n, -1, np.int32)
+        n = ctypes.c_int()
+        tk, u = self._u8(kf_taken, KF.n, 0), self._u8(usable, pts.n)
+        st = self.L.oracle_search_by_projection_sim3(KF.ref(), _p(tk), pts.struct(), _p(u), int(th), _p(out),
+                                                     ctypes.byref(n))
+        assert st == 0
+        return n.value, out
+
+    def SearchBySim3(self, KF1, mp1, usable1, KF2, mp2, usable2, sR12, t12, sR21, t21, th):
+        out = np.full(KF1.n, -1, np.int32)
+        n = ctypes.c_int()
+        u1, u2 = self._u8(usable1, KF1.n), self._u8(usable2, KF2.n)
+        a = [np.ascontiguousarray(np.asarray(x, np.float32).reshape(-1)) for x in (sR12, t12, sR21, t21)]
+        st = self.L.oracle_search_by_sim3(KF1.ref(), mp1.struct(), _p(u1), KF2.ref(), mp2.struct(), _p(u2),
+                                          *map(_p, a), float(th), _p(out), ctypes.byref(n))
+        assert st == 0
+        return n.value, out
+
+    def Fuse(self, KF, pts, usable, th=2.5, scw=False):
+        out = np.full(pts.n, -1, np.int32)
+        n = ctypes.c_int()
+        u = self._u8(usable, pts.n)
+        st = self.L.oracle_fuse(KF.ref(), pts.struct(), _p(u), float(th), int(bool(scw)), _p(out), ctypes.byref(n))
+        assert st == 0
+        return n.value, out
+
+    def GetFeaturesInArea(self, view, x, y, r, min_level=-1, max_level=-1, keyframe=False):
+        out = np.zeros(max(view.n, 1), np.int32)
+        k = self.L.oracle_features_in_area_view(view.ref(), int(keyframe), float(x), float(y), float(r),
+                                                int(min_level), int(max_level), _p(out), len(out))
+        assert k >= 0
+        return out[:k].copy()

@@ -1,0 +1,309 @@
+"""GPU parity of the ORBmatcher family (csrc/orb_match.hip) against the CPU oracle
+(oracle/orb_oracle_match.cpp): identical match arrays and counts, bit for bit, on seeded
+synthetic scenes (tests/scenes.py) that hit every acceptance / rejection branch."""
+import numpy as np
+import pytest
+
+import orbslam_jpminipc_amd as orb
+from orbslam_jpminipc_amd.views import MapPointSet, View
+from oracle_lib import OracleMatcher
+import scenes as S
+
+pytestmark = pytest.mark.gpu
+
+SEEDS = range(6)
+
+
+def both(nnratio=0.6, checkOri=True):
+    return orb.ORBmatcher(nnratio, checkOri), OracleMatcher(nnratio, checkOri)
+
+
+def same(a, b):
+    na, oa = a
+    nb, ob = b
+    assert na == nb, (na, nb)
+    np.testing.assert_array_equal(oa, ob)
+    return na
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+@pytest.mark.parametrize("keyframe", [False, True])
+def test_features_in_area(seed, keyframe):
+    rng = np.random.default_rng(100 + seed)
+    V = S.view(rng, 1500)
+    q = 300
+    x = rng.uniform(-50, S.W + 50, q).astype(np.float32)
+    y = rng.uniform(-50, S.H + 50, q).astype(np.float32)
+    r = rng.uniform(0, 120, q).astype(np.float32)
+    lo = rng.integers(-1, 8, q)
+    hi = np.where(rng.random(q) < 0.3, lo, np.minimum(lo + rng.integers(0, 3, q), 7))
+    hi[lo == -1] = -1
+    g = orb.ORBmatcher.GetFeaturesInArea(V, x, y, r, None if keyframe else lo, None if keyframe else hi, keyframe)
+    o = OracleMatcher()
+    for i in range(q):
+        ref = o.GetFeaturesInArea(V, x[i], y[i], r[i], -1 if keyframe else lo[i], -1 if keyframe else hi[i], keyframe)
+        np.testing.assert_array_equal(g[i], ref)
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_is_in_frustum(seed):
+    rng = np.random.default_rng(200 + seed)
+    T = S.view(rng, 800)
+    mps, _ = S.map_points_on(rng, T, 3000, bad_frac=0.3)
+    g, o = both()
+    for lim in (0.5, 0.0, 0.9):
+        a = g.isInFrustum(T, mps, lim)
+        b = o.isInFrustum(T, mps, lim)
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(x, y)
+    assert a[0].sum() > 0
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+@pytest.mark.parametrize("th", [1.0, 3.0])
+def test_search_by_projection_local(seed, th):
+    rng = np.random.default_rng(300 + seed)
+    F = S.view(rng, 1200)
+    mps, _ = S.map_points_on(rng, F, 2500)
+    g, o = both(0.8)
+    iv, px, py, lv, vc = o.isInFrustum(F, mps, 0.5)
+    taken = (rng.random(F.n) < 0.2).astype(np.uint8)
+    usable = iv & (rng.random(mps.n) < 0.9)
+    n = same(g.SearchByProjection_Local(F, taken, usable, px, py, lv, vc, mps.desc, th),
+             o.SearchByProjection_Local(F, taken, usable, px, py, lv, vc, mps.desc, th))
+    assert n > 0
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+@pytest.mark.parametrize("window,lv", [(100, (0, 2**31 - 1)), (200, (1, 5)), (30, (0, 2**31 - 1))])
+def test_window_search(seed, window, lv):
+    rng = np.random.default_rng(400 + seed)
+    F2 = S.view(rng, 1000, clusters=6, spread=20)
+    idx = rng.integers(0, F2.n, 900)
+    k1 = F2.kps[idx].copy()
+    k1["x"] = np.clip(k1["x"] + rng.normal(0, 4, len(idx)), 0, S.W - 1)
+    k1["y"] = np.clip(k1["y"] + rng.normal(0, 4, len(idx)), 0, S.H - 1)
+    k1["angle"] = (k1["angle"] + rng.choice([0, 0, 0, 90, 200], len(idx))) % 360
+    F1 = View(k1, S.perturb(rng, F2.desc[idx], 80), (0, S.W, 0, S.H))
+    usable = (rng.random(F1.n) < 0.85).astype(np.uint8)
+    for checkOri in (True, False):
+        g, o = both(0.9, checkOri)
+        n = same(g.WindowSearch(F1, usable, F2, window, *lv), o.WindowSearch(F1, usable, F2, window, *lv))
+        assert n > 0
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_search_by_projection_f2f(seed):
+    rng = np.random.default_rng(500 + seed)
+    F2 = S.view(rng, 1000)
+    mps, src = S.map_points_on(rng, F2, 1000, bad_frac=0.1)
+    k1 = S.keypoints(rng, 1000)
+    k1["octave"] = np.where(rng.random(1000) < 0.8, F2.kps["octave"][src], k1["octave"])
+    F1 = View(k1, mps.desc, (0, S.W, 0, S.H))
+    usable = (rng.random(F1.n) < 0.9).astype(np.uint8)
+    taken = (rng.random(F2.n) < 0.15).astype(np.uint8)
+    g, o = both(0.9)
+    for window in (15, 60):
+        n = same(g.SearchByProjection_F2F(F1, mps, usable, F2, taken, window),
+                 o.SearchByProjection_F2F(F1, mps, usable, F2, taken, window))
+        assert n > 0
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_search_by_projection_motion(seed):
+    rng = np.random.default_rng(600 + seed)
+    Cur = S.view(rng, 1200)
+    mps, src = S.map_points_on(rng, Cur, 1000, bad_frac=0.1)
+    k1 = S.keypoints(rng, 1000)
+    k1["octave"] = Cur.kps["octave"][src]
+    k1["angle"] = (Cur.kps["angle"][src] + rng.normal(10, 3, 1000)) % 360
+    Last = View(k1, mps.desc, (0, S.W, 0, S.H))
+    usable = (rng.random(Last.n) < 0.9).astype(np.uint8)
+    taken = (rng.random(Cur.n) < 0.1).astype(np.uint8)
+    for checkOri in (True, False):
+        g, o = both(0.9, checkOri)
+        for th in (7.0, 15.0):
+            n = same(g.SearchByProjection_Motion(Cur, taken, Last, mps, usable, th),
+                     o.SearchByProjection_Motion(Cur, taken, Last, mps, usable, th))
+            assert n > 0
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_search_by_projection_reloc(seed):
+    rng = np.random.default_rng(700 + seed)
+    Cur = S.view(rng, 1200)
+    mps, src = S.map_points_on(rng, Cur, 900, bad_frac=0.1)
+    k = S.keypoints(rng, 900)
+    k["angle"] = (Cur.kps["angle"][src] + rng.normal(-20, 3, 900)) % 360
+    KF = View(k, S.descriptors(rng, 900), (0, S.W, 0, S.H))
+    usable = (rng.random(KF.n) < 0.9).astype(np.uint8)
+    taken = (rng.random(Cur.n) < 0.1).astype(np.uint8)
+    g, o = both(0.9, True)
+    for th, orbdist in ((10, 100), (3, 64)):
+        n = same(g.SearchByProjection_Reloc(Cur, taken, KF, mps, usable, th, orbdist),
+                 o.SearchByProjection_Reloc(Cur, taken, KF, mps, usable, th, orbdist))
+        assert n > 0
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_search_by_projection_sim3(seed):
+    rng = np.random.default_rng(800 + seed)
+    KF = S.view(rng, 1200)
+    pts, _ = S.map_points_on(rng, KF, 1500)
+    usable = (rng.random(pts.n) < 0.9).astype(np.uint8)
+    taken = (rng.random(KF.n) < 0.1).astype(np.uint8)
+    g, o = both()
+    for th in (10, 3):
+        n = same(g.SearchByProjection_Sim3(KF, taken, pts, usable, th),
+                 o.SearchByProjection_Sim3(KF, taken, pts, usable, th))
+        assert n > 0
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+@pytest.mark.parametrize("scw", [False, True])
+def test_fuse(seed, scw):
+    rng = np.random.default_rng(900 + seed)
+    KF = S.view(rng, 1200)
+    pts, _ = S.map_points_on(rng, KF, 2000)
+    usable = (rng.random(pts.n) < 0.9).astype(np.uint8)
+    g, o = both()
+    for th in (3.0, 4.0):
+        n = same(g.Fuse(KF, pts, usable, th, scw), o.Fuse(KF, pts, usable, th, scw))
+        assert n > 0
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_search_by_sim3(seed):
+    rng = np.random.default_rng(1000 + seed)
+    V1, V2, P, i1, i2 = S.two_views_of_points(rng, 600, n_extra=400, kmax=40)
+    m1 = np.zeros((V1.n, 3), np.float32)
+    m2 = np.zeros((V2.n, 3), np.float32)
+    m1[i1] = P
+    m2[i2] = P
+    d1 = V1.desc.copy()
+    d2 = V2.desc.copy()
+
+    def mpset(V, pos, desc, rng):
+        Ow = V.Ow.astype(np.float64)
+        dist = np.linalg.norm(pos - Ow, axis=1)
+        dmin = (dist / S.SF[V.kps["octave"]] * rng.uniform(0.9, 1.1, V.n)).astype(np.float32)
+        return MapPointSet(pos, None, dmin, (dmin * 5.0).astype(np.float32), desc)
+
+    mp1, mp2 = mpset(V1, m1, d1, rng), mpset(V2, m2, d2, rng)
+    u1 = np.zeros(V1.n, np.uint8)
+    u1[i1] = rng.random(len(i1)) < 0.9
+    u2 = np.zeros(V2.n, np.uint8)
+    u2[i2] = rng.random(len(i2)) < 0.9
+    R12, t12 = S.relative_pose(V1, V2)
+    s = np.float32(rng.uniform(0.8, 1.25))
+    # scale the second keyframe's world so that the similarity is not a rigid motion
+    sR12 = (s * R12.astype(np.float32)).astype(np.float32)
+    sR21 = ((1.0 / s) * R12.T.astype(np.float32)).astype(np.float32)
+    t12f = t12.astype(np.float32)
+    t21 = (-(sR21.astype(np.float64) @ t12f.astype(np.float64))).astype(np.float32)
+    g, o = both()
+    for th in (7.5, 15.0):
+        n = same(g.SearchBySim3(V1, mp1, u1, V2, mp2, u2, sR12, t12f, sR21, t21, th),
+                 o.SearchBySim3(V1, mp1, u1, V2, mp2, u2, sR12, t12f, sR21, t21, th))
+    R12f = R12.astype(np.float32)
+    sR21b = R12f.T.copy()
+    t21b = (-(sR21b.astype(np.float64) @ t12f.astype(np.float64))).astype(np.float32)
+    n = same(g.SearchBySim3(V1, mp1, u1, V2, mp2, u2, R12f, t12f, sR21b, t21b, 10.0),
+             o.SearchBySim3(V1, mp1, u1, V2, mp2, u2, R12f, t12f, sR21b, t21b, 10.0))
+    assert n > 0
+
+
+def _bow_pair(rng, n_pts=500, extra=300, share=0.8):
+    V1, V2, P, i1, i2 = S.two_views_of_points(rng, n_pts, n_extra=extra, kmax=45)
+    ids = np.sort(rng.choice(10**6, 80, replace=False))
+    a_pt = rng.integers(0, len(ids), n_pts)
+    a1 = rng.integers(0, len(ids), V1.n)
+    a2 = rng.integers(0, len(ids), V2.n)
+    a1[i1] = a_pt
+    a2[i2] = np.where(rng.random(n_pts) < share, a_pt, rng.integers(0, len(ids), n_pts))
+    # each vector uses only a subset of the nodes
+    keep1 = rng.random(len(ids)) < 0.9
+    keep2 = rng.random(len(ids)) < 0.9
+    a1 = np.where(keep1[a1], a1, np.flatnonzero(keep1)[0])
+    a2 = np.where(keep2[a2], a2, np.flatnonzero(keep2)[0])
+    fv1, _, _ = S.feature_vector(rng, V1.n, node_ids=ids, assign=a1)
+    fv2, _, _ = S.feature_vector(rng, V2.n, node_ids=ids, assign=a2)
+    return V1, V2, fv1, fv2
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_search_by_bow_kf_f(seed):
+    rng = np.random.default_rng(1100 + seed)
+    V1, V2, fv1, fv2 = _bow_pair(rng)
+    usable = (rng.random(V1.n) < 0.8).astype(np.uint8)
+    for nn, co in ((0.75, True), (0.9, False), (0.6, True)):
+        g, o = both(nn, co)
+        n = same(g.SearchByBoW_KF_F(V1, usable, fv1, V2, fv2), o.SearchByBoW_KF_F(V1, usable, fv1, V2, fv2))
+        assert n > 0
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_search_by_bow_kf_kf(seed):
+    rng = np.random.default_rng(1200 + seed)
+    V1, V2, fv1, fv2 = _bow_pair(rng)
+    u1 = (rng.random(V1.n) < 0.8).astype(np.uint8)
+    u2 = (rng.random(V2.n) < 0.8).astype(np.uint8)
+    for nn, co in ((0.75, True), (0.9, False)):
+        g, o = both(nn, co)
+        n = same(g.SearchByBoW_KF_KF(V1, u1, fv1, V2, u2, fv2), o.SearchByBoW_KF_KF(V1, u1, fv1, V2, u2, fv2))
+        assert n > 0
+
+
+@pytest.mark.parametrize("seed", SEEDS)
+def test_search_for_triangulation(seed):
+    rng = np.random.default_rng(1300 + seed)
+    V1, V2, fv1, fv2 = _bow_pair(rng, n_pts=600, extra=200, share=0.9)
+    F12 = S.fundamental12(V1, V2)
+    h1 = (rng.random(V1.n) < 0.3).astype(np.uint8)
+    h2 = (rng.random(V2.n) < 0.3).astype(np.uint8)
+    for co in (True, False):
+        g, o = both(0.6, co)
+        n = same(g.SearchForTriangulation(V1, h1, fv1, V2, h2, fv2, F12),
+                 o.SearchForTriangulation(V1, h1, fv1, V2, h2, fv2, F12))
+        assert n > 0
+
+
+def test_dense_contention_forces_rescans():
+    """Many queries competing for a few dozen targets: every query's top-8 runs out of untaken
+    entries and the resolver's exact rescan path decides (WindowSearch, SBP local, BoW)."""
+    rng = np.random.default_rng(7)
+    k = S.keypoints(rng, 60, clusters=1, spread=6)
+    k["octave"] = 0
+    F2 = View(k, S.descriptors(rng, 60), (0, S.W, 0, S.H))
+    idx = rng.integers(0, 60, 400)
+    k1 = F2.kps[idx].copy()
+    F1 = View(k1, S.perturb(rng, F2.desc[idx], 30), (0, S.W, 0, S.H))
+    g, o = both(0.99, False)
+    n = same(g.WindowSearch(F1, None, F2, 100), o.WindowSearch(F1, None, F2, 100))
+    assert n > 8
+    px, py = k1["x"].copy(), k1["y"].copy()
+    lv = np.zeros(400, np.int32)
+    vc = np.ones(400, np.float32)
+    n = same(g.SearchByProjection_Local(F2, None, None, px, py, lv, vc, F1.desc, 20.0),
+             o.SearchByProjection_Local(F2, None, None, px, py, lv, vc, F1.desc, 20.0))
+    assert n > 8
+    fv1 = S.FeatureVector.from_dict({5: list(range(400))})
+    fv2 = S.FeatureVector.from_dict({5: list(range(60))})
+    n = same(g.SearchByBoW_KF_KF(F1, None, fv1, F2, None, fv2), o.SearchByBoW_KF_KF(F1, None, fv1, F2, None, fv2))
+    n = same(g.SearchByBoW_KF_F(F1, None, fv1, F2, fv2), o.SearchByBoW_KF_F(F1, None, fv1, F2, fv2))
+    assert n > 8
+
+
+def test_empty_inputs():
+    rng = np.random.default_rng(3)
+    F = S.view(rng, 300)
+    E = View(np.zeros(0, orb.KEYPOINT_DTYPE), np.zeros((0, 32), np.uint8), (0, S.W, 0, S.H))
+    g, o = both()
+    assert same(g.WindowSearch(E, None, F, 100), o.WindowSearch(E, None, F, 100)) == 0
+    assert same(g.WindowSearch(F, None, E, 100), o.WindowSearch(F, None, E, 100)) == 0
+    fv = S.FeatureVector.from_dict({})
+    fvF, _, _ = S.feature_vector(rng, F.n)
+    assert same(g.SearchByBoW_KF_F(F, None, fvF, F, fv), o.SearchByBoW_KF_F(F, None, fvF, F, fv)) == 0
+    mps = MapPointSet(np.zeros((0, 3), np.float32), np.zeros((0, 3), np.float32), np.zeros(0, np.float32),
+                      np.zeros(0, np.float32), np.zeros((0, 32), np.uint8))
+    assert same(g.Fuse(F, mps, None), o.Fuse(F, mps, None)) == 0
