@@ -20,6 +20,16 @@ int main() {
     if (ORB_SLAM::gpu::ORBmatcher::DescriptorDistance(a, b) != 256) fails++;
     b[0] = 0;
     if (ORB_SLAM::gpu::ORBmatcher::DescriptorDistance(a, b) != 248) fails++;
+    // matcher family: argument validation happens before any device work
+    orb_frame_view_t v{};
+    v.nlevels = 0;  // invalid
+    std::vector<int> out;
+    try {
+        ORB_SLAM::gpu::ORBmatcher(0.9f, true).WindowSearch(v, nullptr, v, 100, out);
+        fails++;
+    } catch (const std::runtime_error& e) {
+        if (!std::strstr(e.what(), "status -22")) fails++;
+    }
     std::printf("facade fails %d\n", fails);
     return fails;
 }

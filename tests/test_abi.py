@@ -91,3 +91,29 @@ def test_cpp_facade_compiles_and_fails_loudly():
                     f"-L{pkg}", "-lorb_hip", f"-Wl,-rpath,{pkg}", "-Wl,-rpath-link,/opt/rocm/lib"], check=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_matcher_family_validates_before_device_work():
+    """Bad views, flag arrays and FeatureVectors fail with ORB_EINVAL/ENOTSUP on any host."""
+    from orbslam_jpminipc_amd.views import FeatureVector, View
+
+    k = np.zeros(3, orb.KEYPOINT_DTYPE)
+    k["octave"] = [0, 1, 9]  # octave 9 >= nlevels
+    V = View(k, np.zeros((3, 32), np.uint8))
+    m = orb.ORBmatcher(0.9, True)
+    with pytest.raises(orb.OrbError) as e:
+        m.WindowSearch(V, None, V, 100)
+    assert e.value.code == _native.ORB_EINVAL
+    k["octave"] = 0
+    V = View(k, np.zeros((3, 32), np.uint8), bounds=(0, 0, 0, 480))  # empty bounds
+    with pytest.raises(orb.OrbError):
+        m.WindowSearch(V, None, V, 100)
+    V = View(k, np.zeros((3, 32), np.uint8))
+    bad = FeatureVector([5, 3], [0, 1, 2], [0, 1])  # node ids not ascending
+    good = FeatureVector([3, 5], [0, 1, 3], [0, 1, 2])
+    with pytest.raises(orb.OrbError) as e:
+        m.SearchByBoW_KF_KF(V, None, bad, V, None, good)
+    assert e.value.code == _native.ORB_EINVAL
+    oob = FeatureVector([3], [0, 1], [7])  # feature index out of range
+    with pytest.raises(orb.OrbError):
+        m.SearchByBoW_KF_F(V, None, oob, V, good)
