@@ -440,10 +440,45 @@ struct ScoreGreater {  // KeypointResponseGreater on the packed FAST score
 // (ORBextractor.cc:680-701) — exact libstdc++ nth_element replays.  Lists live in LDS when the
 // level's survivors fit (SELECT_CAP), otherwise in the frame's scratch area `cand2`.
 #define SELECT_CAP 6144
+// KeypointResponseGreater on HARRIS_SCORE elements: float response in the high word, the
+// packed FAST record (identity) in the low word.
+struct HarrisGreater {
+    __device__ bool operator()(uint64_t a, uint64_t b) const {
+        return __uint_as_float((uint32_t)(a >> 32)) > __uint_as_float((uint32_t)(b >> 32));
+    }
+};
+
+// HarrisResponses (ORBextractor.cc:79-120) at level pixel (x, y), blockSize 7, k = 0.04:
+// cellImage is a view into the level, so the 7x7 block starts at (x-3, y-3) of the level.
+// g++ -O3 -march=native contracts the response to fma(-(k*s), s, fma(A, B, -(C*C))) (oracle
+// harris_responses, DESIGN.md §FP policy).
+__device__ __forceinline__ float harris_response(const uint8_t* roi, int pitch, int x, int y, float scale4) {
+    const uint8_t* p0 = roi + (long long)(y - 3) * pitch + (x - 3);
+    int a = 0, b = 0, c = 0;
+    for (int i = 0; i < 7; ++i)
+#pragma unroll
+        for (int j = 0; j < 7; ++j) {
+            const uint8_t* ptr = p0 + (long long)i * pitch + j;
+            const int Ix = (ptr[1] - ptr[-1]) * 2 + (ptr[-pitch + 1] - ptr[-pitch - 1]) + (ptr[pitch + 1] - ptr[pitch - 1]);
+            const int Iy = (ptr[pitch] - ptr[-pitch]) * 2 + (ptr[pitch - 1] - ptr[-pitch - 1]) + (ptr[pitch + 1] - ptr[-pitch + 1]);
+            a += Ix * Ix;
+            b += Iy * Iy;
+            c += Ix * Iy;
+        }
+    const float fa = (float)a, fb = (float)b, fc = (float)c;
+    const float s = fa + fb;
+    const float t3 = 0.04f * s;
+    const float u = __builtin_fmaf(fa, fb, -(fc * fc));
+    const float rsp = __builtin_fmaf(-t3, s, u);
+    return rsp * scale4;
+}
+
+template <bool HARRIS>
 __global__ void __launch_bounds__(256) k_select(const uint8_t* __restrict__ pyr, uint32_t* __restrict__ cand,
                                                 uint32_t* __restrict__ cand2, int* __restrict__ cellCount, Geom g,
                                                 const CellGeom* __restrict__ cells, uint32_t* __restrict__ lvlOut,
-                                                int* __restrict__ lvlCount) {
+                                                int* __restrict__ lvlCount, uint64_t* __restrict__ candH,
+                                                float* __restrict__ lvlResp, float harrisScale4) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ int s_cnt[ORB_MAX_CELLS_PER_LEVEL];
     __shared__ int s_ret[ORB_MAX_CELLS_PER_LEVEL];
@@ -563,6 +598,65 @@ __global__ void __launch_bounds__(256) k_select(const uint8_t* __restrict__ pyr,
         }
     }
     __syncthreads();
+    if constexpr (HARRIS) {
+        // HarrisResponses on every cell keypoint (ORBextractor.cc:616-620), then the same
+        // retention on (response, record) pairs
+        uint64_t* hs = inLds ? (uint64_t*)(smem + (size_t)8 * SELECT_CAP) : candH + (long long)b * g.candPerFrame;
+        const uint8_t* roi = pyr + lg.base + (long long)b * lg.fstride + (long long)EDGE * lg.pitch + EDGE;
+        for (int c = wave; c < nC; c += 4) {
+            const int o = inLds ? s_off[c] : lc[c].candOff;
+            for (int i = lane; i < s_cnt[c]; i += 64) {
+                const uint32_t e = srt[o + i];
+                const float r = harris_response(roi, lg.pitch, e & 0xFFF, (e >> 12) & 0xFFF, harrisScale4);
+                hs[o + i] = ((uint64_t)__float_as_uint(r) << 32) | e;
+            }
+        }
+        __syncthreads();
+        HarrisGreater hcomp;
+        for (int c = tid; c < nC; c += 256) {
+            uint64_t* seg = hs + (inLds ? s_off[c] : lc[c].candOff);
+            s_cnt[c] = orbsel::retain_best(seg, s_cnt[c], s_ret[c], hcomp);
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int s = 0;
+            for (int c = 0; c < nC; ++c) {
+                s_koff[c] = s;
+                s += s_cnt[c];
+            }
+            s_koff[nC] = s;
+        }
+        __syncthreads();
+        const int K = s_koff[nC];
+        uint64_t* list;
+        if (inLds) {  // kept prefixes of hs -> the raw + srt region (disjoint)
+            list = (uint64_t*)smem;
+            for (int c = wave; c < nC; c += 4)
+                for (int k = lane; k < s_cnt[c]; k += 64) list[s_koff[c] + k] = hs[s_off[c] + k];
+        } else {
+            list = hs + lc[0].candOff;
+            if (tid == 0)
+                for (int c = 0; c < nC; ++c) {
+                    const uint64_t* src = hs + lc[c].candOff;
+                    for (int k = 0; k < s_cnt[c]; ++k) list[s_koff[c] + k] = src[k];
+                }
+        }
+        __syncthreads();
+        int keep = K;
+        if (K > lg.nDesired) {
+            keep = lg.nDesired;
+            if (tid == 0) orbsel::retain_best(list, K, lg.nDesired, hcomp);
+        }
+        __syncthreads();
+        const long long ob = (long long)b * g.kpCap + lg.kpBase;
+        for (int k = tid; k < keep; k += 256) {
+            const uint64_t v = list[k];
+            lvlOut[ob + k] = (uint32_t)v;
+            lvlResp[ob + k] = __uint_as_float((uint32_t)(v >> 32));
+        }
+        if (tid == 0) lvlCount[(long long)b * g.L + l] = keep;
+        return;
+    }
     // (4) retainBest per cell, then the level list in cell order, then retainBest to the quota
     ScoreGreater comp;
     for (int c = tid; c < nC; c += 256) {
@@ -937,7 +1031,8 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
                                                      const uint8_t* __restrict__ blur, Geom g,
                                                      const uint32_t* __restrict__ lvlOut,
                                                      const int* __restrict__ lvlCount, orb_keypoint_t* __restrict__ kps,
-                                                     uint8_t* __restrict__ desc, int* __restrict__ counts) {
+                                                     uint8_t* __restrict__ desc, int* __restrict__ counts,
+                                                     const float* __restrict__ lvlResp) {
     __shared__ __attribute__((aligned(16))) uint32_t s_patch[4][31 * IC_P / 4];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int b = blockIdx.y;
@@ -998,7 +1093,13 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
     float sa, ca;
     glibc_sincosf(angle * factorPI, &sa, &ca);
     const float a = ca, bsin = sa;
-    const uint8_t* center = blur + fbase + (long long)(y + EDGE) * lg.pitch + (x + EDGE);
+    // samples inside the level ROI read the blur, samples in the padding the raw reflect-101
+    // border (the reference blurs the ROI in place, ORBextractor.cc:760).  Keypoints of
+    // non-last cells can sit past maxBorder (ORBextractor.cc:560-597), so the 18-px reach can
+    // leave the 3-px ring k_level materialises: select per sample.
+    const long long coff = (long long)(y + EDGE) * lg.pitch + (x + EDGE);
+    const uint8_t* center = blur + fbase + coff;
+    const uint8_t* rawc = pyr + fbase + coff;
     const int pitch = lg.pitch;
     int vals[8];
 #pragma unroll
@@ -1007,7 +1108,8 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
         const float px = (float)c_pattern[2 * pt], py = (float)c_pattern[2 * pt + 1];
         const int dy = (int)rintf(__builtin_fmaf(px, bsin, py * a));
         const int dx = (int)rintf(__builtin_fmaf(px, a, -(py * bsin)));
-        vals[q] = center[(long long)dy * pitch + dx];
+        const bool roi = (unsigned)(x + dx) < (unsigned)lg.w && (unsigned)(y + dy) < (unsigned)lg.h;
+        vals[q] = (roi ? center : rawc)[(long long)dy * pitch + dx];
     }
     int nib = 0;
 #pragma unroll
@@ -1021,7 +1123,7 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
         kp.y = l == 0 ? (float)y : (float)y * lg.scale;
         kp.size = lg.size;
         kp.angle = angle;
-        kp.response = (float)score;
+        kp.response = lvlResp ? lvlResp[(long long)b * g.kpCap + lg.kpBase + idx] : (float)score;
         kp.octave = l;
         kp.class_id = -1;
         kps[kslot] = kp;
@@ -1392,6 +1494,9 @@ struct orb_extractor {
     uint32_t* d_cand2 = nullptr;  // k_select scratch when a level's survivors exceed its LDS
     uint32_t* d_lvl = nullptr;
     int* d_lvlCount = nullptr;
+    uint64_t* d_candH = nullptr;  // HARRIS_SCORE: (response, record) scratch when a level exceeds LDS
+    float* d_lvlResp = nullptr;   // HARRIS_SCORE: response of every kept keypoint
+    float harrisScale4 = 0.f;
     int* d_rtab = nullptr;
     CellGeom* d_cells = nullptr;
     // per-stage HIP-event timing (orb_profile_*): stage k brackets its kernel(s) on the launch stream
@@ -1424,6 +1529,8 @@ struct orb_extractor {
         hipFree(d_cand2);
         hipFree(d_lvl);
         hipFree(d_lvlCount);
+        hipFree(d_candH);
+        hipFree(d_lvlResp);
         hipFree(d_rtab);
         hipFree(d_cells);
         hipFree(d_img);
@@ -1439,6 +1546,8 @@ struct orb_extractor {
         d_cand2 = nullptr;
         d_lvl = nullptr;
         d_lvlCount = nullptr;
+        d_candH = nullptr;
+        d_lvlResp = nullptr;
         d_rtab = nullptr;
         d_cells = nullptr;
         d_img = nullptr;
@@ -1587,7 +1696,7 @@ struct orb_extractor {
                 }
             }
         }
-        selectLds = std::max(cellLds, (size_t)2 * SELECT_CAP * 4);
+        selectLds = std::max(cellLds, (size_t)(scoreType == ORB_HARRIS_SCORE ? 4 : 2) * SELECT_CAP * 4);
         if (selectLds > 150 * 1024) return set_err(ORB_ENOTSUP, "FAST cell larger than the LDS budget");
         // resize tables, l >= 1
         for (int l = 1; l < nlevels; ++l) {
@@ -1680,6 +1789,10 @@ struct orb_extractor {
         HIP_TRY(hipMalloc(&d_cand2, (size_t)std::max(cand, 1) * maxBatch * 4));
         HIP_TRY(hipMalloc(&d_lvl, (size_t)std::max(kpCap, 1) * maxBatch * 4));
         HIP_TRY(hipMalloc(&d_lvlCount, (size_t)nlevels * maxBatch * 4));
+        if (scoreType == ORB_HARRIS_SCORE) {
+            HIP_TRY(hipMalloc(&d_candH, (size_t)std::max(cand, 1) * maxBatch * 8));
+            HIP_TRY(hipMalloc(&d_lvlResp, (size_t)std::max(kpCap, 1) * maxBatch * 4));
+        }
         HIP_TRY(hipMalloc(&d_rtab, std::max<size_t>(rt.size(), 1) * 4));
         HIP_TRY(hipMalloc(&d_cells, cl.size() * sizeof(CellGeom)));
         if (!rt.empty()) HIP_TRY(hipMemcpy(d_rtab, rt.data(), rt.size() * 4, hipMemcpyHostToDevice));
@@ -1760,13 +1873,17 @@ struct orb_extractor {
                            d_cellCount);
         stage_end(st);
         stage_begin(3, st);
-        hipLaunchKernelGGL(k_select, dim3(nlevels, B), dim3(256), selectLds, st, d_pyr, d_cand, d_cand2, d_cellCount, g,
-                           d_cells, d_lvl, d_lvlCount);
+        if (scoreType == ORB_HARRIS_SCORE)
+            hipLaunchKernelGGL(k_select<true>, dim3(nlevels, B), dim3(256), selectLds, st, d_pyr, d_cand, d_cand2,
+                               d_cellCount, g, d_cells, d_lvl, d_lvlCount, d_candH, d_lvlResp, harrisScale4);
+        else
+            hipLaunchKernelGGL(k_select<false>, dim3(nlevels, B), dim3(256), selectLds, st, d_pyr, d_cand, d_cand2,
+                               d_cellCount, g, d_cells, d_lvl, d_lvlCount, (uint64_t*)nullptr, (float*)nullptr, 0.f);
         stage_end(st);
         stage_begin(4, st);
         dim3 gd((std::max(kpCap, 1) + 3) / 4, B);
         hipLaunchKernelGGL(k_orient_desc, gd, dim3(256), 0, st, d_pyr, d_blur, g, d_lvl, d_lvlCount, kps, desc,
-                           counts);
+                           counts, (const float*)d_lvlResp);
         stage_end(st);
         HIP_TRY(hipGetLastError());
         return ORB_OK;
@@ -1800,19 +1917,25 @@ int orb_extractor_create(int nfeatures, float scale_factor, int nlevels, int sco
         return set_err(ORB_EINVAL, "invalid extractor parameters");
     if (score_type != ORB_FAST_SCORE && score_type != ORB_HARRIS_SCORE)
         return set_err(ORB_EINVAL, "score_type must be HARRIS_SCORE(0) or FAST_SCORE(1)");
-    if (score_type == ORB_HARRIS_SCORE) return set_err(ORB_ENOTSUP, "HARRIS_SCORE is not implemented on the GPU path yet");
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
     if (device < 0 || device >= ndev) return set_err(ORB_EINVAL, "device ordinal out of range");
     HIP_TRY(hipSetDevice(device));
     int st = upload_pattern(device);
     if (st) return st;
+    // k_select<true> (HARRIS_SCORE) stages (response, record) pairs: up to 96 KB of LDS
+    hipFuncSetAttribute((const void*)k_select<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
     orb_extractor* h = new orb_extractor();
     h->nfeatures = nfeatures;
     h->scaleFactor = scale_factor;
     h->nlevels = nlevels;
     h->scoreType = score_type;
     h->fastTh = fast_th;
+    {  // HarrisResponses' scale (ORBextractor.cc:89-91), blockSize 7, in the reference's float steps
+        float scale = (1 << 2) * 7 * 255.0f;
+        scale = 1.0f / scale;
+        h->harrisScale4 = scale * scale * scale * scale;
+    }
     h->device = device;
     h->maxBatch = max_batch;
     h->init_params();

@@ -87,10 +87,12 @@ def test_extract_parity_odd_sizes(W, H):
 
 
 @pytest.mark.parametrize("W,H,nf,nl,th", [(161, 121, 2000, 4, 20), (160, 120, 2000, 4, 7), (128, 96, 1500, 5, 12),
-                                           (200, 150, 2000, 3, 20), (176, 144, 2000, 3, 7)])
+                                           (200, 150, 2000, 3, 20), (176, 144, 2000, 3, 7), (161, 121, 2000, 8, 7),
+                                           (161, 121, 3000, 8, 20)])
 def test_extract_parity_dense_cell_grids(W, H, nf, nl, th):
     """Many small cells: the ceil'd cell size makes the non-last cells' detection areas reach
-    past maxBorder (ORBextractor.cc:572-597), so FAST runs beyond h-16 / w-16 there."""
+    past maxBorder (ORBextractor.cc:572-597), so FAST runs beyond h-16 / w-16 there and the
+    rBRIEF samples of such keypoints reach past the 3-px descriptor ring into raw padding."""
     ext = orb.ORBextractor(nf, 1.2, nl, orb.FAST_SCORE, th, device=0)
     ora = Oracle(nf, 1.2, nl, 1, th)
     for img in orb.synth_stream(W, H, stream=17, first=0, count=2):
@@ -233,3 +235,44 @@ def test_match_batch_device_parity():
         no, m12o = search_for_initialization(k1, desc_h[p, :n1], k2, desc_h[p + 1, :n2], W, H, prev, 0.9, True, 100)
         assert nm[p] == no
         assert np.array_equal(m12[p, :n1], m12o)
+
+
+@pytest.mark.parametrize("W,H,nf,th", [(640, 480, 1000, 20), (1241, 376, 2000, 20), (320, 240, 500, 12),
+                                       (161, 121, 2000, 7)])
+def test_extract_parity_harris_score(W, H, nf, th):
+    """scoreType = HARRIS_SCORE (ORBextractor.cc:616-620): Harris responses (float) drive both
+    retainBest passes and land in KeyPoint::response."""
+    ext = orb.ORBextractor(nf, 1.2, 8, orb.HARRIS_SCORE, th, device=0)
+    ora = Oracle(nf, 1.2, 8, 0, th)
+    for img in orb.synth_stream(W, H, stream=11, first=0, count=2):
+        kg, _ = _check_frame(ext, ora, img)
+        assert len(kg) and not np.all(kg["response"] == np.round(kg["response"]))  # float responses
+
+
+@pytest.mark.parametrize("kind", [orb.SYN_LOWTEX, orb.SYN_NOISE])
+def test_extract_parity_harris_edge_frames(kind):
+    ext = orb.ORBextractor(1000, 1.2, 8, orb.HARRIS_SCORE, 20, device=0)
+    ora = Oracle(1000, 1.2, 8, 0, 20)
+    _check_frame(ext, ora, orb.synth_special(kind, 640, 480, seed=5))
+
+
+def test_harris_batch_device_equals_single():
+    import torch
+
+    W, H, B = 640, 480, 6
+    frames = orb.synth_stream(W, H, stream=2, first=0, count=B)
+    ext = orb.ORBextractor(1000, 1.2, 8, orb.HARRIS_SCORE, 20, device=0, max_batch=B)
+    cap = ext.max_keypoints
+    d_k = torch.empty((B, cap, 28), dtype=torch.uint8, device="cuda")
+    d_d = torch.empty((B, cap, 32), dtype=torch.uint8, device="cuda")
+    d_c = torch.empty((B,), dtype=torch.int32, device="cuda")
+    ext.extract_batch_device(torch.from_numpy(frames).cuda(), d_k, d_d, d_c)
+    torch.cuda.synchronize()
+    ora = Oracle(1000, 1.2, 8, 0, 20)
+    cnt = d_c.cpu().numpy()
+    kh, dh = d_k.cpu().numpy(), d_d.cpu().numpy()
+    for b in range(B):
+        ko, do = ora.extract(frames[b])
+        assert cnt[b] == len(ko)
+        assert kh[b, :cnt[b]].tobytes() == ko.tobytes()
+        assert dh[b, :cnt[b]].tobytes() == do.tobytes()
