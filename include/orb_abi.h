@@ -292,7 +292,8 @@ int orb_debug_nth_element_u32(uint32_t* a, int n, int nth);
 /* Padded pyramid level l of batch frame b after the last extraction (device sync). */
 int orb_debug_level_image(orb_extractor_t* h, int b, int l, uint8_t* out, int* w, int* hgt);
 /* Descriptor image (blurred ROI + un-blurred padding ring) of level l, frame b, padded
- * (w+32) x (h+32) layout; only the ring [-3, w+3) x [-3, h+3) is defined (device sync). */
+ * (w+32) x (h+32) layout; defined over [-3, w+3) x [-3, h+3) at least (wider where a dense
+ * cell grid lets keypoints sit past the FAST border) (device sync). */
 int orb_debug_blur_image(orb_extractor_t* h, int b, int l, uint8_t* out);
 /* Per-cell FAST keypoint counts of frame b, level l (device sync); returns #cells. */
 int orb_debug_cell_counts(orb_extractor_t* h, int b, int l, int* counts, int cap);

@@ -34,7 +34,18 @@
 
 #define ORB_MAX_LEVELS 16
 #define ORB_MAX_CELLS_PER_LEVEL 256
-#define ORB_SELECT_LDS_CAP 6144  // level list kept in LDS when it fits (u32 entries)
+#define ORB_SELECT_LDS_CAP 6144
+// k_level phase switches: timing experiments only (scripts/klevel_phases.sh builds variants
+// with -DKL_SKIP_*=1 into build/variants); the product build leaves them 0.
+#ifndef KL_SKIP_BLUR
+#define KL_SKIP_BLUR 0
+#endif
+#ifndef KL_SKIP_FAST
+#define KL_SKIP_FAST 0
+#endif
+#ifndef KL_SKIP_QUEUE
+#define KL_SKIP_QUEUE 0
+#endif  // level list kept in LDS when it fits (u32 entries)
 
 // ======================================================================================
 // error plumbing
@@ -74,6 +85,8 @@ struct LevelGeom {
     float size;             // (int)(31 * mvScaleFactor[l])
     int cellW, cellH;       // detection-area size of the (non-last) cells: corner -> cell bucket
     int detX1, detY1;       // FAST detection region [16, detX1) x [16, detY1): union of the cells' areas
+    int ringX1, ringY1;     // descriptor image defined over [-3, ringX1) x [-3, ringY1): every rBRIEF
+                            // sample (reach 18) of a keypoint in the detection region
 };
 
 struct Geom {
@@ -702,9 +715,9 @@ __global__ void __launch_bounds__(256) k_select(const uint8_t* __restrict__ pyr,
 // ---- descriptor image: GaussianBlur(level ROI, 7x7, sigma 2) in place ---------------------
 // The reference blurs the level ROI in place right before its descriptors
 // (ORBextractor.cc:760): samples inside the ROI read the blur, samples in the 16-px padding
-// read the un-blurred reflect-101 border (rBRIEF reaches 2 px into it).  k_level materialises
-// exactly that image over level coordinates [-3, w+3) x [-3, h+3) in a buffer laid out like
-// the pyramid.  Fixed-point taps (18,34,49,55,49,34,18)/256 per axis:
+// read the un-blurred reflect-101 border.  k_level materialises exactly that image over level
+// coordinates [-3, ringX1) x [-3, ringY1) (all a keypoint's samples can reach: 3 px past the
+// ROI, more where non-last cells extend past maxBorder) in a buffer laid out like the pyramid.  Fixed-point taps (18,34,49,55,49,34,18)/256 per axis:
 // T = sum_j k_j sum_i k_i P; columns x < 4*floor(w/4) round T/65536 half-to-even (the SSE2
 // SymmColumnVec_32s8u float path), the tail columns half-up ((T + 2^15) >> 16).
 #define BLUR_TW 256  // output columns per tile: 64 lanes x 4 pixels
@@ -837,7 +850,7 @@ __global__ void __launch_bounds__(256) k_level(const uint8_t* __restrict__ pyr, 
         const bool in = lane < 2 * nr && X >= EDGE && X < lg.detX1 && Y >= EDGE && Y < lg.detY1;
         push(in ? (right ? 1u : 8u) : 0u, rt, right ? 65 : 0);
     }
-    const bool colLive = x < lg.w + 4;
+    const bool colLive = x < lg.ringX1;
     const bool lanePlain = x >= 0 && x + 3 < lg.xsimd_blur;  // all 4 px inside the ROI, SSE2 columns
     const uint32_t* in = s_in + (wave * BLUR_RW + 1) * BLUR_IW + lane;
     f32x2 R[7][2];  // horizontal sums of the ring rows, pixels (0,1) and (2,3)
@@ -864,13 +877,13 @@ __global__ void __launch_bounds__(256) k_level(const uint8_t* __restrict__ pyr, 
             if (r < 6) continue;
             const int rt = wave * BLUR_RW + (r - 6);  // output row (tile); ring slot (k+4)%7 is its centre
             const int y = t.y0 + rt;
-            if (y >= lg.h + 3) {
+            if (y >= lg.ringY1) {
                 done = true;
                 break;
             }
             const int kc = (k + 4) % 7, km1 = (k + 3) % 7, kp1 = (k + 5) % 7, km2 = (k + 2) % 7, kp2 = (k + 6) % 7,
                       km3 = (k + 1) % 7;
-            if (colLive) {
+            if (colLive && !KL_SKIP_BLUR) {
                 uint32_t word;
                 if (y >= 0 && y < lg.h) {
                     f32x2 v[2];
@@ -910,7 +923,7 @@ __global__ void __launch_bounds__(256) k_level(const uint8_t* __restrict__ pyr, 
                 *(uint32_t*)(dst + (long long)(y + EDGE) * lg.pitch + (x + EDGE)) = word;
             }
             // FAST pre-filter for the row (wave-uniform row test)
-            if (y >= EDGE && y < lg.detY1) {
+            if (!KL_SKIP_FAST && y >= EDGE && y < lg.detY1) {
                 const uint32_t cc = C[kc];
                 const uint32_t* ic = in + (r - 3) * BLUR_IW;  // centre row in LDS
                 const uint32_t a4 = __builtin_amdgcn_alignbyte(ic[2], cc, 3);   // x+3 .. x+6
@@ -924,7 +937,7 @@ __global__ void __launch_bounds__(256) k_level(const uint8_t* __restrict__ pyr, 
     {
         const int TP = BLUR_IW * 4;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        for (int i0 = 0; i0 < qn; i0 += 64) {
+        for (int i0 = 0; i0 < (KL_SKIP_QUEUE ? 0 : qn); i0 += 64) {
             const int i = i0 + lane;
             const uint32_t e = i < qn ? pq[i] : 0u;
             const int rt = rBase + (int)(e >> 11), cb = 4 * ((int)((e >> 4) & 127) - 1);
@@ -1093,13 +1106,8 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
     float sa, ca;
     glibc_sincosf(angle * factorPI, &sa, &ca);
     const float a = ca, bsin = sa;
-    // samples inside the level ROI read the blur, samples in the padding the raw reflect-101
-    // border (the reference blurs the ROI in place, ORBextractor.cc:760).  Keypoints of
-    // non-last cells can sit past maxBorder (ORBextractor.cc:560-597), so the 18-px reach can
-    // leave the 3-px ring k_level materialises: select per sample.
-    const long long coff = (long long)(y + EDGE) * lg.pitch + (x + EDGE);
-    const uint8_t* center = blur + fbase + coff;
-    const uint8_t* rawc = pyr + fbase + coff;
+    // the descriptor image covers every sample a keypoint of this level can reach (ringX1/Y1)
+    const uint8_t* center = blur + fbase + (long long)(y + EDGE) * lg.pitch + (x + EDGE);
     const int pitch = lg.pitch;
     int vals[8];
 #pragma unroll
@@ -1108,8 +1116,7 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
         const float px = (float)c_pattern[2 * pt], py = (float)c_pattern[2 * pt + 1];
         const int dy = (int)rintf(__builtin_fmaf(px, bsin, py * a));
         const int dx = (int)rintf(__builtin_fmaf(px, a, -(py * bsin)));
-        const bool roi = (unsigned)(x + dx) < (unsigned)lg.w && (unsigned)(y + dy) < (unsigned)lg.h;
-        vals[q] = (roi ? center : rawc)[(long long)dy * pitch + dx];
+        vals[q] = center[(long long)dy * pitch + dx];
     }
     int nib = 0;
 #pragma unroll
@@ -1645,6 +1652,12 @@ struct orb_extractor {
             lg.cellH = cellH;
             lg.detX1 = std::max(maxBX, levelCols > 1 ? 16 + (levelCols - 1) * cellW : 0);
             lg.detY1 = std::max(maxBY, levelRows > 1 ? 16 + (levelRows - 1) * cellH : 0);
+            // keypoints of non-last cells can sit past maxBorder (ORBextractor.cc:560-597); the
+            // descriptor image must hold every sample they reach (|offset| <= 18)
+            lg.ringX1 = std::max(lg.w + 3, lg.detX1 + 18);
+            lg.ringY1 = std::max(lg.h + 3, lg.detY1 + 18);
+            if (lg.ringX1 > lg.w + 12 || lg.ringY1 > lg.h + 12)
+                return set_err(ORB_ENOTSUP, "cell grid too dense: rBRIEF samples leave the 16-px padding");
             if (cellW <= 0 || cellH <= 0) return set_err(ORB_ENOTSUP, "empty cell size");
             lg.cell0 = (int)cl.size();
             std::vector<int> iniXCol(levelCols, 0);
@@ -1779,8 +1792,8 @@ struct orb_extractor {
         HIP_TRY(hipMalloc(&d_blur, (size_t)pyrBytes));
         std::vector<BlurTile> tl;
         for (int l = 0; l < nlevels; ++l)
-            for (int y0 = -3; y0 < G.lv[l].h + 3; y0 += BLUR_TH)
-                for (int x0 = -4; x0 < G.lv[l].w + 4; x0 += BLUR_TW) tl.push_back(BlurTile{l, x0, y0});
+            for (int y0 = -3; y0 < G.lv[l].ringY1; y0 += BLUR_TH)
+                for (int x0 = -4; x0 < G.lv[l].ringX1; x0 += BLUR_TW) tl.push_back(BlurTile{l, x0, y0});
         HIP_TRY(hipMalloc(&d_tiles, tl.size() * sizeof(BlurTile)));
         HIP_TRY(hipMemcpy(d_tiles, tl.data(), tl.size() * sizeof(BlurTile), hipMemcpyHostToDevice));
         nTiles = (int)tl.size();

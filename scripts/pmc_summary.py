@@ -1,19 +1,57 @@
 #!/usr/bin/env python3
-"""Average rocprofv3 PMC counters per kernel over all passes of scripts/pmc_pass.sh."""
+"""Per-kernel HBM bytes per launch from the rocprofv3 PMC passes of scripts/pmc_pass.sh.
+
+Usage: pmc_summary.py gpurun_out/TAG [--json OUT] [--width W --height H --batch B --nfeatures N]
+
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch (TCC_EA0 request counters, MI355X_MICROARCH.md
+§HBM).  The guide's ×2 FETCH correction is calibrated for 16-B/lane streaming loads only; the
+extraction kernels load dwords, so the read calibration is measured in the same run: k_pyr0
+reads exactly the B input frames (B·W·H bytes, evicted from the 256 MiB Infinity Cache by the
+~0.6 GB every step writes) with the same dword-per-lane pattern, and read_bytes = FETCH ×
+(B·W·H / FETCH(k_pyr0)) for every kernel.  WRITE_SIZE is taken as is (exact for streaming
+stores per the guide).
+"""
+import argparse
 import csv
 import glob
-import sys
+import json
 from collections import defaultdict
 
-root = sys.argv[1]
-acc = defaultdict(lambda: defaultdict(list))
-for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
-    for r in csv.DictReader(open(f)):
-        name = r["Kernel_Name"].split("(")[0]
-        acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
-for k, d in acc.items():
-    if k.startswith("__amd") or "elementwise" in k:
-        continue
-    print(k)
-    for c, v in sorted(d.items()):
-        print(f"   {c:24s} {sum(v) / len(v):16.4g}  (n={len(v)})")
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("root")
+    ap.add_argument("--json")
+    ap.add_argument("--width", type=int, default=640)
+    ap.add_argument("--height", type=int, default=480)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--nfeatures", type=int, default=1000)
+    a = ap.parse_args()
+    acc = defaultdict(lambda: defaultdict(list))
+    for f in sorted(glob.glob(f"{a.root}/p*/run_counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            name = r["Kernel_Name"].split("(")[0].split("<")[0].replace("void ", "")
+            acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    mean = {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in acc.items()
+            if not k.startswith("__amd") and "elementwise" not in k and "at::" not in k}
+    known = a.batch * a.width * a.height
+    cal = known / (mean["k_pyr0"]["FETCH_SIZE"] * 1024.0) if "k_pyr0" in mean else None
+    out = {"workload": {"width": a.width, "height": a.height, "batch": a.batch, "nfeatures": a.nfeatures},
+           "read_calibration": {"kernel": "k_pyr0", "known_read_bytes": known, "factor": cal},
+           "per_launch": {}}
+    for k, d in sorted(mean.items()):
+        if "FETCH_SIZE" not in d or "WRITE_SIZE" not in d:
+            continue
+        rd = d["FETCH_SIZE"] * 1024.0 * (cal or 1.0)
+        wr = d["WRITE_SIZE"] * 1024.0
+        out["per_launch"][k] = {"fetch_kib": d["FETCH_SIZE"], "write_kib": d["WRITE_SIZE"], "read_bytes": rd,
+                                "write_bytes": wr, "hbm_bytes": rd + wr,
+                                **{c: v for c, v in d.items() if c.startswith("SQ_")}}
+        print(f"{k:16s} read {rd / 1e6:10.2f} MB  write {wr / 1e6:10.2f} MB  per launch")
+    print(f"read calibration factor (k_pyr0): {cal}")
+    if a.json:
+        json.dump(out, open(a.json, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
