@@ -116,19 +116,22 @@ def main():
     d_cnt = torch.empty((B,), dtype=torch.int32, device="cuda")
     f1 = torch.arange(0, B - 1, dtype=torch.int32, device="cuda")
     f2 = f1 + 1
-    stream = torch.cuda.current_stream()
+    # one stream carries the whole step: extraction, then the matching that reads its output
+    stream = torch.cuda.Stream()
+    torch.cuda.current_stream().synchronize()  # inputs uploaded on the default stream
     ev_m = []
 
     def step(timed=False):
-        ext.extract_batch_device(d_imgs, d_kps, d_desc, d_cnt, stream=stream)
-        if timed:
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record(stream)
-        m12, nm = matcher.search_for_initialization_batch_device(d_kps, d_desc, d_cnt, f1, f2, W, H, 100,
-                                                                 stream=stream)
-        if timed:
-            b.record(stream)
-            ev_m.append((a, b))
+        with torch.cuda.stream(stream):
+            ext.extract_batch_device(d_imgs, d_kps, d_desc, d_cnt, stream=stream)
+            if timed:
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(stream)
+            m12, nm = matcher.search_for_initialization_batch_device(d_kps, d_desc, d_cnt, f1, f2, W, H, 100,
+                                                                     stream=stream)
+            if timed:
+                b.record(stream)
+                ev_m.append((a, b))
         return nm
 
     for _ in range(args.warmup):

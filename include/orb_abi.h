@@ -87,8 +87,10 @@ int orb_extract(orb_extractor_t* h, const uint8_t* img, int w, int hgt, int stri
  *   d_imgs: B frames, frame k at d_imgs + k*frame_pitch, each w x h at row pitch `stride`.
  *   d_kps: B x cap records, cap = orb_get_max_keypoints(h) (frame k at d_kps + k*cap);
  *   d_desc: B x cap x 32 bytes; d_counts: B int32 keypoint counts.
- *   stream: hipStream_t to enqueue on (NULL = the handle's own stream).  Asynchronous:
- *   returns after enqueueing; synchronise the stream before reading outputs. */
+ *   stream: hipStream_t to enqueue on (NULL = the null stream, as in every HIP API; the
+ *   handle's own stream serves only the host-buffer entry points).  Asynchronous: returns
+ *   after enqueueing; work on other streams must be ordered against it by the caller
+ *   (events), and the stream synchronised before reading outputs. */
 int orb_extract_batch_device(orb_extractor_t* h, int B, const uint8_t* d_imgs, int w, int hgt, int stride,
                              int64_t frame_pitch, orb_keypoint_t* d_kps, uint8_t* d_desc, int32_t* d_counts,
                              void* stream);
@@ -274,6 +276,52 @@ int orb_search_by_sim3(const orb_frame_view_t* KF1, orb_map_points_t mp1, const 
  * applies Replace / AddObservation in point order (the map mutation stays on the host). */
 int orb_fuse(const orb_frame_view_t* KF, orb_map_points_t pts, const uint8_t* usable, float th, int scw,
              int32_t* best_idx, int* n_fused, int device);
+
+/* ---- DBoW2 vocabulary (GPU: csrc/orb_voc.hip) -------------------------------------- */
+/* The reference's ORBVocabulary = DBoW2::TemplatedVocabulary<FORB::TDescriptor, FORB>
+ * (include/ORBVocabulary.h).  A handle holds the tree on `device`; host entry points are
+ * serialised per handle, device entry points enqueue on the caller's stream.
+ * Weighting: 0 TF_IDF, 1 TF, 2 IDF, 3 BINARY; scoring: 0 L1_NORM, 1 L2_NORM, 2 CHI_SQUARE,
+ * 3 KL, 4 BHATTACHARYYA, 5 DOT_PRODUCT (BowVector.h:36-53). */
+typedef struct orb_vocabulary orb_vocabulary_t; /* opaque handle */
+
+/* TemplatedVocabulary::loadFromTextFile (TemplatedVocabulary.h:1338-1424): header
+ * "k L scoring weighting", then one line per node "parent isLeaf d0 .. d31 weight".
+ * Blank lines are skipped; a malformed line or a parent that does not
+ * precede its child is ORB_EINVAL (the reference reads such files unchecked). */
+int orb_vocabulary_load_text(const char* path, int device, orb_vocabulary_t** out);
+/* The same tree from arrays: node i + 1 (i < n_nodes) has parent[i] (<= i), is_leaf[i],
+ * desc[32 i .. 32 i + 31] and weight[i], i.e. the lines of the text format in order. */
+int orb_vocabulary_create(int k, int L, int scoring, int weighting, int n_nodes, const int32_t* parent,
+                          const uint8_t* is_leaf, const uint8_t* desc, const double* weight, int device,
+                          orb_vocabulary_t** out);
+int orb_vocabulary_destroy(orb_vocabulary_t* v);
+/* info[7] = k, L, scoring, weighting, nodes (root included), words, tree height. */
+int orb_vocabulary_info(const orb_vocabulary_t* v, int32_t* info);
+
+/* transform(feature, word_id, weight, &nid, levelsup) (TemplatedVocabulary.h:1217-1259) for
+ * n device descriptors (32 B rows, 16-B aligned): word id, weight and the node at level
+ * L - levelsup (the root when that level is <= 0).  Asynchronous on `stream`. */
+int orb_vocabulary_transform_features_device(const orb_vocabulary_t* v, int n, const uint8_t* d_desc, int levelsup,
+                                             uint32_t* d_word, double* d_weight, uint32_t* d_node, void* stream);
+
+/* transform(features, BowVector, FeatureVector, levelsup) (TemplatedVocabulary.h:1126-1194) for
+ * B frames laid out as orb_extract_batch_device writes them (frame b: d_desc + b*cap*32,
+ * d_counts[b] rows).  Per frame, capacity cap each: d_feat_* per-feature results (as above);
+ * BowVector = d_bow_words / d_bow_values[d_bow_n[b]] in ascending word order; FeatureVector
+ * = CSR d_fv_nodes[d_fv_n[b]], d_fv_offsets (cap + 1 per frame), d_fv_features.  cap <= 8192.
+ * Asynchronous on `stream`. */
+int orb_vocabulary_transform_batch_device(const orb_vocabulary_t* v, int B, const uint8_t* d_desc,
+                                          const int32_t* d_counts, int cap, int levelsup, uint32_t* d_feat_word,
+                                          double* d_feat_weight, uint32_t* d_feat_node, uint32_t* d_bow_words,
+                                          double* d_bow_values, int32_t* d_bow_n, uint32_t* d_fv_nodes,
+                                          int32_t* d_fv_offsets, int32_t* d_fv_features, int32_t* d_fv_n,
+                                          void* stream);
+
+/* The same for one frame of n host descriptors (synchronous); outputs sized n (offsets n + 1). */
+int orb_vocabulary_transform(orb_vocabulary_t* v, const uint8_t* desc, int n, int levelsup, uint32_t* bow_words,
+                             double* bow_values, int* bow_n, uint32_t* fv_nodes, int32_t* fv_offsets,
+                             int32_t* fv_features, int* fv_n);
 
 /* ---- measurement ------------------------------------------------------------------- */
 /* Per-stage HIP-event timing of the extraction kernels: when enabled, every

@@ -120,6 +120,21 @@ int oracle_search_for_triangulation(const orb_frame_view_t* KF1, const uint8_t* 
                                     const float* F12, float nnratio, int check_ori, int32_t* match12,
                                     int* n_matches);
 
+/* ---- orb_oracle_voc.cpp: DBoW2 vocabulary (TemplatedVocabulary.h:1126-1259, 1338-1424) --- */
+typedef struct oracle_vocabulary oracle_vocabulary_t;
+oracle_vocabulary_t* oracle_vocabulary_load_text(const char* path);
+oracle_vocabulary_t* oracle_vocabulary_create(int k, int L, int scoring, int weighting, int n_nodes,
+                                              const int32_t* parent, const uint8_t* is_leaf, const uint8_t* desc,
+                                              const double* weight);
+void oracle_vocabulary_destroy(oracle_vocabulary_t* v);
+/* info[6] = k, L, scoring, weighting, nodes (root included), words */
+int oracle_vocabulary_info(const oracle_vocabulary_t* v, int32_t* info);
+int oracle_vocabulary_transform_one(const oracle_vocabulary_t* v, const uint8_t* desc, int levelsup, uint32_t* word,
+                                    double* weight, uint32_t* nid);
+int oracle_vocabulary_transform(const oracle_vocabulary_t* v, const uint8_t* desc, int n, int levelsup,
+                                uint32_t* bow_words, double* bow_values, int* bow_n, uint32_t* fv_nodes,
+                                int32_t* fv_offsets, int32_t* fv_features, int* fv_n);
+
 #ifdef __cplusplus
 }
 #endif

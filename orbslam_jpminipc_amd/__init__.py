@@ -15,10 +15,12 @@ from ._native import (
 from .extractor import ORBextractor, keypoints_from_bytes
 from .matcher import Frame, ORBmatcher
 from .synth import SYN_FLAT, SYN_LOWTEX, SYN_NOISE, SYN_SCENE, synth_special, synth_stream
+from .vocabulary import ORBVocabulary
 
 __all__ = [
     "ORBextractor",
     "ORBmatcher",
+    "ORBVocabulary",
     "Frame",
     "KEYPOINT_DTYPE",
     "FAST_SCORE",

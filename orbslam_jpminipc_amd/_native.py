@@ -138,6 +138,16 @@ HIP_SIGNATURES = {
     "orb_search_by_projection_sim3": (_i, [_pv, _vp, MapPoints, _vp, _i, _vp, _pi, _i]),
     "orb_search_by_sim3": (_i, [_pv, MapPoints, _vp, _pv, MapPoints, _vp, _vp, _vp, _vp, _vp, _f, _vp, _pi, _i]),
     "orb_fuse": (_i, [_pv, MapPoints, _vp, _f, _i, _vp, _pi, _i]),
+    "orb_vocabulary_load_text": (_i, [ctypes.c_char_p, _i, ctypes.POINTER(_vp)]),
+    "orb_vocabulary_create": (_i, [_i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _i, ctypes.POINTER(_vp)]),
+    "orb_vocabulary_destroy": (_i, [_vp]),
+    "orb_vocabulary_info": (_i, [_vp, _vp]),
+    "orb_vocabulary_transform_features_device": (_i, [_vp, _i, _vp, _i, _vp, _vp, _vp, _vp]),
+    "orb_vocabulary_transform_batch_device": (
+        _i,
+        [_vp, _i, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    ),
+    "orb_vocabulary_transform": (_i, [_vp, _vp, _i, _i, _vp, _vp, _pi, _vp, _vp, _vp, _pi]),
     "orb_profile_enable": (_i, [_vp, _i]),
     "orb_profile_read": (_i, [_vp, _vp, _vp, _i]),
     "orb_profile_stage_name": (ctypes.c_char_p, [_i]),

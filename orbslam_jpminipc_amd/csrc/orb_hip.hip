@@ -137,29 +137,66 @@ __global__ void __launch_bounds__(256) k_pyr0(const uint8_t* __restrict__ imgs, 
     *(uint32_t*)(pyr + lg.base + (long long)b * lg.fstride + (long long)py * lg.pitch + x4) = word;
 }
 
-// ---- global -> LDS staging --------------------------------------------------------------
 // Copy `rows` rows of `words` dwords (global row stride gsw words, LDS row stride lsw words)
 // with 256 threads: waves take rows, lanes take words, and every thread issues up to 8
-// independent loads before its LDS stores, so a workgroup pays a few memory latencies
-// instead of one per row.  Words at or beyond `wlimit` in a row are not read (stay 0).
-__device__ __forceinline__ void stage_rows_to_lds(uint32_t* __restrict__ dst, int lsw,
-                                                  const uint32_t* __restrict__ src, long long gsw, int rows,
-                                                  int words, int wlimit, int wave, int lane) {
+// independent loads before its LDS stores (k_pyr_resize's narrow, tall source tiles).
+__device__ __forceinline__ void stage_rows_by_wave(uint32_t* __restrict__ dst, int lsw,
+                                                   const uint32_t* __restrict__ src, long long gsw, int rows,
+                                                   int words, int wave, int lane) {
     for (int wx0 = 0; wx0 < words; wx0 += 64) {
         const int wx = wx0 + lane;
         const bool colok = wx < words;
-        const bool inb = wx < wlimit;
         for (int r0 = wave; r0 < rows; r0 += 32) {
             uint32_t v[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 const int r = r0 + 4 * k;
-                v[k] = (colok && inb && r < rows) ? src[(long long)r * gsw + wx] : 0u;
+                v[k] = (colok && r < rows) ? src[(long long)r * gsw + wx] : 0u;
             }
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 const int r = r0 + 4 * k;
                 if (colok && r < rows) dst[r * lsw + wx] = v[k];
+            }
+        }
+    }
+}
+
+// Stage `rows` x `words` dwords (global row pitch gsw dwords, columns >= wlimit read as 0)
+// into LDS (row pitch lsw dwords).  The block issues all its loads of a batch (SB per thread)
+// before any LDS write, so a tile costs one memory round trip instead of one per row group
+// (k_level's wide tiles).
+#define SB 20
+__device__ __forceinline__ void stage_rows_to_lds(uint32_t* __restrict__ dst, int lsw,
+                                                  const uint32_t* __restrict__ src, long long gsw, int rows,
+                                                  int words, int wlimit, int tid) {
+    const int total = rows * words;
+    const int dr = 256 / words, dc = 256 - dr * words;
+    for (int base = 0; base < total; base += SB * 256) {
+        const int i0 = base + tid;
+        const int r0 = i0 / words, c0 = i0 - r0 * words;
+        uint32_t v[SB];
+        int r = r0, c = c0;
+#pragma unroll
+        for (int k = 0; k < SB; ++k) {
+            v[k] = (base + k * 256 + tid < total && c < wlimit) ? src[(long long)r * gsw + c] : 0u;
+            r += dr;
+            c += dc;
+            if (c >= words) {
+                c -= words;
+                ++r;
+            }
+        }
+        r = r0;
+        c = c0;
+#pragma unroll
+        for (int k = 0; k < SB; ++k) {
+            if (base + k * 256 + tid < total) dst[r * lsw + c] = v[k];
+            r += dr;
+            c += dc;
+            if (c >= words) {
+                c -= words;
+                ++r;
             }
         }
     }
@@ -184,8 +221,8 @@ __global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, c
     const int* tt = rtab + lg.rtile + 4 * (blockIdx.y * gridDim.x + blockIdx.x);
     const int colStart = tt[0], words = tt[1], rowMin = tt[2], nrows = tt[3];
     const uint8_t* S = pyr + ls.base + (long long)b * ls.fstride + (long long)EDGE * ls.pitch + EDGE;
-    stage_rows_to_lds(s_src, words, (const uint32_t*)(S + (long long)rowMin * ls.pitch + colStart), ls.pitch >> 2,
-                      nrows, words, words, wave, lane);
+    stage_rows_by_wave(s_src, words, (const uint32_t*)(S + (long long)rowMin * ls.pitch + colStart), ls.pitch >> 2,
+                       nrows, words, wave, lane);
     const int* xofs = rtab + lg.rtab;
     const int* alpha = xofs + lg.w;
     const int* yofs = alpha + lg.w;
@@ -814,7 +851,7 @@ __global__ void __launch_bounds__(256) k_level(const uint8_t* __restrict__ pyr, 
     const int rows = min(BLUR_TH + 8, lg.ph - py0);
     const int spw = lg.pitch >> 2;
     stage_rows_to_lds(s_in, BLUR_IW, (const uint32_t*)(src + (long long)py0 * lg.pitch + px0), spw, rows, BLUR_IW,
-                      spw - (px0 >> 2), wave, lane);
+                      spw - (px0 >> 2), tid);
     for (int i = tid; i < (BLUR_TH + 2) * LVL_SPW / 4; i += 256) ((uint32_t*)s_S)[i] = 0u;
     __syncthreads();
     const uint8_t* inb = (const uint8_t*)s_in;
@@ -1183,21 +1220,20 @@ __global__ void __launch_bounds__(256) k_match_init(const orb_keypoint_t* __rest
     const uint32_t* D1 = (const uint32_t*)(desc + (long long)f1 * cap * 32);
     const uint32_t* D2 = (const uint32_t*)(desc + (long long)f2 * cap * 32);
     uint32_t* s_d2 = (uint32_t*)smem;              // nmax x 8
-    float* s_x2 = (float*)(s_d2 + (size_t)nmax * 8);
+    // per F2 slot: x = vMatchedDistance (low 16 bits, 0xFFFF = INT_MAX) | (vnMatches21 + 1) << 16,
+    // y = the F2 keypoint index — one LDS read gives the greedy pass all it needs of a slot
+    uint2* s_st = (uint2*)(s_d2 + (size_t)nmax * 8);
+    float* s_x2 = (float*)(s_st + nmax);
     float* s_y2 = s_x2 + nmax;
     int* s_cell = (int*)(s_y2 + nmax);              // posX * 48 + posY
-    int* s_idx = s_cell + nmax;                     // i2
-    int* s_md = s_idx + nmax;                       // vMatchedDistance
-    int* s_m21 = s_md + nmax;                       // vnMatches21
-    int* s_q2i = s_m21 + nmax;                      // query -> i1
+    int* s_q2i = s_cell + nmax;                     // query -> i1
     float* s_qx = (float*)(s_q2i + nmax);
     float* s_qy = s_qx + nmax;
-    float* s_qa = s_qy + nmax;                      // query angle
-    float* s_a2 = s_qa + nmax;                      // F2 slot angle
+    float* s_a2 = s_qy + nmax;                      // F2 slot angle
     uint32_t* s_list = (uint32_t*)(s_a2 + nmax);    // nmax x TOPK
     int* s_lcnt = (int*)(s_list + (size_t)nmax * MATCH_TOPK);
     int* s_m12 = s_lcnt + nmax;                     // vnMatches12 (cap)
-    signed char* s_bin = (signed char*)(s_m12 + cap);  // rotation bin of accepted i1 (cap)
+    short* s_bslot = (short*)(s_m12 + cap);         // F2 slot of each accepted i1, then its rotation bin (cap)
     uint32_t* s_key = s_list;                       // phase-0 scratch (cap <= 8 * nmax)
     const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     // ---- phase 0: keys in parallel, then ordered compaction from LDS ----
@@ -1250,9 +1286,7 @@ __global__ void __launch_bounds__(256) k_match_init(const orb_keypoint_t* __rest
         s_y2[rank] = kp.y;
         s_a2[rank] = kp.angle;
         s_cell[rank] = (int)(k >> 16);
-        s_idx[rank] = i2;
-        s_md[rank] = 0x7fffffff;
-        s_m21[rank] = -1;
+        s_st[rank] = make_uint2(0xFFFFu, (uint32_t)i2);
 #pragma unroll
         for (int w = 0; w < 8; ++w) s_d2[rank * 8 + w] = D2[(long long)i2 * 8 + w];
     }
@@ -1261,12 +1295,11 @@ __global__ void __launch_bounds__(256) k_match_init(const orb_keypoint_t* __rest
         const orb_keypoint_t kp = K1[i1];
         s_qx[q] = prev ? prev[((long long)p * cap + i1) * 2] : kp.x;
         s_qy[q] = prev ? prev[((long long)p * cap + i1) * 2 + 1] : kp.y;
-        s_qa[q] = kp.angle;
     }
     __syncthreads();
     for (int i = tid; i < n1; i += 256) {
         s_m12[i] = -1;
-        s_bin[i] = -1;
+        s_bslot[i] = -1;
     }
     __syncthreads();
     // ---- phase 1: per-query top-8 (dist, order) ----
@@ -1307,24 +1340,37 @@ __global__ void __launch_bounds__(256) k_match_init(const orb_keypoint_t* __rest
         }
     }
     __syncthreads();
-    // ---- phase 2: the sequential greedy pass (ORBmatcher.cc:611-680) ----
-    if (wave == 0) {
+    // ---- phase 2: the sequential greedy pass (ORBmatcher.cc:611-680) on one wave ----
+    // Per query the critical path is one LDS read of its top-8 slots' state and scalar lane
+    // reads (v_readlane: no LDS round trip); the next query's list is fetched while this one
+    // resolves, and the rotation bins are computed afterwards, in parallel (phase 3).
+    if (wave == 0 && n1c > 0) {
+        int cntN = s_lcnt[0], i1N = s_q2i[0];
+        uint32_t eN = lane < MATCH_TOPK ? s_list[lane] : 0xFFFFFFFFu;
         for (int q = 0; q < n1c; ++q) {
-            const int cnt = s_lcnt[q];
+            const int cnt = cntN, i1 = i1N;
+            const uint32_t e = eN;
+            if (q + 1 < n1c) {
+                cntN = s_lcnt[q + 1];
+                i1N = s_q2i[q + 1];
+                eN = lane < MATCH_TOPK ? s_list[(q + 1) * MATCH_TOPK + lane] : 0xFFFFFFFFu;
+            }
             if (cnt == 0) continue;  // vIndices2.empty()
-            const int i1 = s_q2i[q];
             const int k = min(cnt, MATCH_TOPK);
-            const uint32_t e = lane < k ? s_list[q * MATCH_TOPK + lane] : 0xFFFFFFFFu;
-            const bool valid = lane < k && s_md[e & 0x7FF] > (int)(e >> 11);
-            uint64_t m = __ballot(valid);
-            uint32_t best;
+            const uint2 st = lane < k ? s_st[e & 0x7FF] : make_uint2(0u, 0u);
+            const bool valid = lane < k && (int)(st.x & 0xFFFFu) > (int)(e >> 11);
+            const uint64_t m = __ballot(valid);
+            uint32_t best, bst, bidx;
             int second;
             if (__popcll(m) >= 2 || cnt <= MATCH_TOPK) {
                 if (m == 0) continue;  // every candidate already held at <= its distance
                 const int e1 = __ffsll((unsigned long long)m) - 1;
-                best = __shfl(e, e1, 64);
+                best = (uint32_t)__builtin_amdgcn_readlane((int)e, e1);
+                bst = (uint32_t)__builtin_amdgcn_readlane((int)st.x, e1);
+                bidx = (uint32_t)__builtin_amdgcn_readlane((int)st.y, e1);
                 const uint64_t m2 = m & (m - 1);
-                second = m2 ? (int)(__shfl(e, __ffsll((unsigned long long)m2) - 1, 64) >> 11) : 0x7fffffff;
+                second = m2 ? (int)((uint32_t)__builtin_amdgcn_readlane((int)e, __ffsll((unsigned long long)m2) - 1) >> 11)
+                            : 0x7fffffff;
             } else {
                 // exact rescan of the whole window
                 const float qx = s_qx[q], qy = s_qy[q];
@@ -1343,7 +1389,7 @@ __global__ void __launch_bounds__(256) k_match_init(const orb_keypoint_t* __rest
                     if (cx < minCX || cx > maxCX || cy < minCY || cy > maxCY) continue;
                     if (fabsf(s_x2[j] - qx) > r || fabsf(s_y2[j] - qy) > r) continue;
                     const int dist = hamming256(d1, s_d2 + j * 8);
-                    if (s_md[j] <= dist) continue;
+                    if ((int)(s_st[j].x & 0xFFFFu) <= dist) continue;
                     const uint32_t key = ((uint32_t)dist << 11) | (uint32_t)j;
                     if (key < lb) {
                         if (lb != 0xFFFFFFFFu) ls = (int)(lb >> 11);
@@ -1361,27 +1407,22 @@ __global__ void __launch_bounds__(256) k_match_init(const orb_keypoint_t* __rest
                 for (int o = 32; o >= 1; o >>= 1) contrib = min(contrib, __shfl_xor(contrib, o, 64));
                 best = gb;
                 second = contrib;
+                const uint2 sb = s_st[gb & 0x7FF];
+                bst = sb.x;
+                bidx = sb.y;
             }
             const int bestDist = (int)(best >> 11);
             const int bestSlot = (int)(best & 0x7FF);
             if (bestDist <= 50 && (float)bestDist < (float)second * nnratio) {
+                // one wave: its LDS accesses complete in issue order, so lane 0's writes are
+                // seen by the next query's reads
                 if (lane == 0) {
-                    const int bestIdx2 = s_idx[bestSlot];
-                    const int old = s_m21[bestSlot];
+                    const int old = (int)(bst >> 16) - 1;  // vnMatches21[bestIdx2]
                     if (old >= 0) s_m12[old] = -1;
-                    s_m12[i1] = bestIdx2;
-                    s_m21[bestSlot] = i1;
-                    s_md[bestSlot] = bestDist;
-                    if (checkOri) {
-                        float rot = s_qa[q] - s_a2[bestSlot];
-                        if (rot < 0.0f) rot += 360.0f;
-                        int bin = (int)roundf(rot * (1.0f / 30));
-                        if (bin == 30) bin = 0;
-                        s_bin[i1] = (signed char)bin;
-                    }
+                    s_m12[i1] = (int)bidx;
+                    s_st[bestSlot].x = (uint32_t)bestDist | ((uint32_t)(i1 + 1) << 16);
+                    s_bslot[i1] = (short)bestSlot;
                 }
-                // lane 0's LDS writes land before any lane's next read (same wave, in order)
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             }
         }
     }
@@ -1390,8 +1431,17 @@ __global__ void __launch_bounds__(256) k_match_init(const orb_keypoint_t* __rest
     if (checkOri) {
         if (tid < 32) s_hist[tid] = 0;
         __syncthreads();
-        for (int i = tid; i < n1; i += 256)
-            if (s_bin[i] >= 0) atomicAdd(&s_hist[(int)s_bin[i]], 1);
+        // rotation bin of every accepted i1, the stolen ones included (ORBmatcher.cc:664-676)
+        for (int i = tid; i < n1; i += 256) {
+            const int sl = s_bslot[i];
+            if (sl < 0) continue;
+            float rot = K1[i].angle - s_a2[sl];
+            if (rot < 0.0f) rot += 360.0f;
+            int bin = (int)roundf(rot * (1.0f / 30));
+            if (bin == 30) bin = 0;
+            s_bslot[i] = (short)bin;
+            atomicAdd(&s_hist[bin], 1);
+        }
         __syncthreads();
         if (tid == 0) {  // ComputeThreeMaxima (ORBmatcher.cc:1748-1789)
             int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
@@ -1427,7 +1477,7 @@ __global__ void __launch_bounds__(256) k_match_init(const orb_keypoint_t* __rest
         __syncthreads();
         const int i1x = s_ind[0], i2x = s_ind[1], i3x = s_ind[2];
         for (int i = tid; i < n1; i += 256) {
-            const int bn = s_bin[i];
+            const int bn = s_bslot[i];
             if (bn >= 0 && bn != i1x && bn != i2x && bn != i3x) s_m12[i] = -1;
         }
         __syncthreads();
@@ -1483,7 +1533,8 @@ struct orb_extractor {
     std::vector<int> nDesired;
     int umax[16] = {};
     int kpCap = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;      // the handle's own stream (host-buffer entry points)
+    hipStream_t lastStream = nullptr;  // stream of the last orb_extract_batch_device
     // geometry of the current frame size
     int W = 0, H = 0;
     Geom g{};
@@ -1995,12 +2046,15 @@ int orb_extract_batch_device(orb_extractor_t* h, int B, const uint8_t* d_imgs, i
     if (w <= 0 || hgt <= 0 || stride < w || frame_pitch < (int64_t)stride * hgt)
         return set_err(ORB_EINVAL, "bad image geometry");
     HIP_TRY(hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;  // NULL = the null stream, as everywhere in HIP
     if (w != h->W || hgt != h->H) {
+        // the workspace is re-allocated: drain every stream that may still be using it
         HIP_TRY(hipStreamSynchronize(h->stream));
-        int st = h->build_geometry(w, hgt);
-        if (st) return st;
+        HIP_TRY(hipStreamSynchronize(h->lastStream));
+        int r = h->build_geometry(w, hgt);
+        if (r) return r;
     }
-    hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+    h->lastStream = st;
     return h->launch(B, d_imgs, stride, frame_pitch, d_kps, d_desc, d_counts, st);
 }
 
@@ -2064,9 +2118,9 @@ int orb_descriptor_distance(const uint8_t* a, const uint8_t* b) {
 }
 
 static size_t match_lds_bytes(int cap, int nmax) {
-    // F2 slots (desc 32 + x,y,a,cell,idx,md,m21 28) + queries (q2i,qx,qy,qa 16 + top-8 32 + cnt 4)
-    // + cap x (m12 4 + bin 1)
-    return (size_t)nmax * (56 + 56) + (size_t)cap * 5 + 16;
+    // F2 slots (desc 32 + state 8 + x,y,a,cell 16) + queries (q2i,qx,qy 12 + top-8 32 + cnt 4)
+    // + cap x (m12 4 + slot/bin 2)
+    return (size_t)nmax * (56 + 48) + (size_t)cap * 6 + 16;
 }
 
 int orb_search_for_initialization_batch_device(const orb_keypoint_t* d_kps, const uint8_t* d_desc,
