@@ -277,6 +277,46 @@ int orb_search_by_sim3(const orb_frame_view_t* KF1, orb_map_points_t mp1, const 
 int orb_fuse(const orb_frame_view_t* KF, orb_map_points_t pts, const uint8_t* usable, float th, int scw,
              int32_t* best_idx, int* n_fused, int device);
 
+/* ---- the front end over a camera stream, overlapped (csrc/orb_pipeline.hip) ---------- */
+/* B consecutive frames of one camera: ORBextractor::operator() on each (Frame::Frame,
+ * Frame.cc:56-128) and SearchForInitialization(F_b, F_b+1) for b < B-1 with vbPrevMatched =
+ * F_b's keypoints (Tracking.cc:366-368, 392-393).  The batch is cut into n_streams contiguous
+ * chunks, each with its own extractor handle and HIP stream, so latency-bound kernels of
+ * one chunk overlap the others; outputs equal the serial path's.  One handle = one caller. */
+typedef struct orb_pipeline orb_pipeline_t; /* opaque handle */
+int orb_pipeline_create(int nfeatures, float scale_factor, int nlevels, int score_type, int fast_th, int device,
+                        int max_batch, int n_streams, orb_pipeline_t** out);
+int orb_pipeline_destroy(orb_pipeline_t* p);
+int orb_pipeline_max_keypoints(const orb_pipeline_t* p);
+int orb_pipeline_streams(const orb_pipeline_t* p);
+/* Outputs as orb_extract_batch_device (d_kps/d_desc/d_counts, per-frame capacity
+ * orb_pipeline_max_keypoints) and orb_search_for_initialization_batch_device (pair b = (b, b+1):
+ * d_matches12 (B-1) x cap, d_nmatches B-1).  Ordered after earlier work on `stream` and
+ * before later work on it (events); asynchronous. */
+int orb_pipeline_extract_and_match(orb_pipeline_t* p, int B, const uint8_t* d_imgs, int w, int hgt, int stride,
+                                   int64_t frame_pitch, orb_keypoint_t* d_kps, uint8_t* d_desc, int32_t* d_counts,
+                                   orb_frame_bounds_t bounds, float nnratio, int check_ori, int window,
+                                   int32_t* d_matches12, int32_t* d_nmatches, void* stream);
+/* Per-stage HIP-event timing summed over the chunk handles (see orb_profile_*). */
+int orb_pipeline_profile_enable(orb_pipeline_t* p, int enable);
+int orb_pipeline_profile_read(orb_pipeline_t* p, double* stage_ms, int64_t* stage_launches, int nstages);
+
+/* ---- MapPoint descriptor maintenance (GPU: csrc/orb_mappoint.hip) ------------------- */
+/* MapPoint::ComputeDistinctiveDescriptors (reference src/MapPoint.cc:185-250) for M points:
+ * point m's observed descriptors are rows offsets[m] .. offsets[m+1]-1 of desc (32 B each), in
+ * the order of its std::map<KeyFrame*, size_t> observations; usable[r] = !pKF->isBad() for the
+ * keyframe of row r (NULL = all).  best_row[m] = the row chosen as mDescriptor and
+ * out_desc[m] = its bytes, or best_row[m] = -1 and out_desc[m] untouched when no row is usable
+ * (the reference returns without changing mDescriptor).  <= 4000 rows per point.
+ * Host buffers, synchronous. */
+int orb_compute_distinctive_descriptors(int M, const int32_t* offsets, const uint8_t* desc, const uint8_t* usable,
+                                        int32_t* best_row, uint8_t* out_desc, int device);
+/* The same on device buffers (desc 16-B aligned); max_obs = the largest row count of a point.
+ * Asynchronous on `stream`. */
+int orb_compute_distinctive_descriptors_device(int M, const int32_t* d_offsets, const uint8_t* d_desc,
+                                               const uint8_t* d_usable, int max_obs, int32_t* d_best_row,
+                                               uint8_t* d_out_desc, void* stream);
+
 /* ---- DBoW2 vocabulary (GPU: csrc/orb_voc.hip) -------------------------------------- */
 /* The reference's ORBVocabulary = DBoW2::TemplatedVocabulary<FORB::TDescriptor, FORB>
  * (include/ORBVocabulary.h).  A handle holds the tree on `device`; host entry points are

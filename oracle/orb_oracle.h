@@ -120,6 +120,10 @@ int oracle_search_for_triangulation(const orb_frame_view_t* KF1, const uint8_t* 
                                     const float* F12, float nnratio, int check_ori, int32_t* match12,
                                     int* n_matches);
 
+/* ---- orb_oracle_mappoint.cpp: MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:185-250) */
+int oracle_compute_distinctive_descriptors(int M, const int32_t* offsets, const uint8_t* desc, const uint8_t* usable,
+                                           int32_t* best_row, uint8_t* out_desc);
+
 /* ---- orb_oracle_voc.cpp: DBoW2 vocabulary (TemplatedVocabulary.h:1126-1259, 1338-1424) --- */
 typedef struct oracle_vocabulary oracle_vocabulary_t;
 oracle_vocabulary_t* oracle_vocabulary_load_text(const char* path);

@@ -138,6 +138,18 @@ HIP_SIGNATURES = {
     "orb_search_by_projection_sim3": (_i, [_pv, _vp, MapPoints, _vp, _i, _vp, _pi, _i]),
     "orb_search_by_sim3": (_i, [_pv, MapPoints, _vp, _pv, MapPoints, _vp, _vp, _vp, _vp, _vp, _f, _vp, _pi, _i]),
     "orb_fuse": (_i, [_pv, MapPoints, _vp, _f, _i, _vp, _pi, _i]),
+    "orb_pipeline_create": (_i, [_i, _f, _i, _i, _i, _i, _i, _i, ctypes.POINTER(_vp)]),
+    "orb_pipeline_destroy": (_i, [_vp]),
+    "orb_pipeline_max_keypoints": (_i, [_vp]),
+    "orb_pipeline_streams": (_i, [_vp]),
+    "orb_pipeline_extract_and_match": (
+        _i,
+        [_vp, _i, _vp, _i, _i, _i, _i64, _vp, _vp, _vp, FrameBounds, _f, _i, _i, _vp, _vp, _vp],
+    ),
+    "orb_pipeline_profile_enable": (_i, [_vp, _i]),
+    "orb_pipeline_profile_read": (_i, [_vp, _vp, _vp, _i]),
+    "orb_compute_distinctive_descriptors": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _i]),
+    "orb_compute_distinctive_descriptors_device": (_i, [_i, _vp, _vp, _vp, _i, _vp, _vp, _vp]),
     "orb_vocabulary_load_text": (_i, [ctypes.c_char_p, _i, ctypes.POINTER(_vp)]),
     "orb_vocabulary_create": (_i, [_i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _i, ctypes.POINTER(_vp)]),
     "orb_vocabulary_destroy": (_i, [_vp]),

@@ -839,6 +839,7 @@ __global__ void __launch_bounds__(256) k_level(const uint8_t* __restrict__ pyr, 
     __shared__ __attribute__((aligned(16))) uint8_t s_S[(BLUR_TH + 2) * LVL_SPW];
     __shared__ uint16_t s_pq[4][LVL_FQ];
     __shared__ uint16_t s_cq[4][LVL_CQ];
+    __shared__ uint16_t s_px[4][LVL_CQ];  // queue entries expanded to pixels (<= 4 x 64)
     const BlurTile t = tiles[blockIdx.x];
     const int b = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const LevelGeom& lg = g.lv[t.level];
@@ -860,6 +861,7 @@ __global__ void __launch_bounds__(256) k_level(const uint8_t* __restrict__ pyr, 
     const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint16_t* pq = s_pq[wave];
     uint16_t* cq = s_cq[wave];
+    uint16_t* px = s_px[wave];
     const int x = t.x0 + 4 * lane;  // first of this lane's 4 columns
     const int rBase = wave * BLUR_RW - 1;  // tile row of rowCode 0
     // detection-region columns of this lane (4-bit mask, lane constant)
@@ -978,13 +980,27 @@ __global__ void __launch_bounds__(256) k_level(const uint8_t* __restrict__ pyr, 
             const int i = i0 + lane;
             const uint32_t e = i < qn ? pq[i] : 0u;
             const int rt = rBase + (int)(e >> 11), cb = 4 * ((int)((e >> 4) & 127) - 1);
-            int cn = 0;
+            // expand the 64 lane-row entries into one pixel per slot (order is irrelevant: the
+            // corners land in the strength plane), so the 9-arc test runs with every lane busy
+            int np = 0;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
+                const bool v = (e >> j) & 1u;
+                const uint64_t m = __ballot(v);
+                if (v) px[np + __popcll(m & below)] = (uint16_t)(((rt + 1) << 9) | (cb + j + 1));
+                np += __popcll(m);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            int cn = 0;
+            for (int p0 = 0; p0 < np; p0 += 64) {
                 bool corner = false;
-                if ((e >> j) & 1u) corner = fast_is_corner(inb + (rt + 4) * TP + cb + j + 4, TP, ft);
+                uint16_t c = 0;
+                if (p0 + lane < np) {
+                    c = px[p0 + lane];
+                    corner = fast_is_corner(inb + ((c >> 9) + 3) * TP + (c & 511) + 3, TP, ft);
+                }
                 const uint64_t m = __ballot(corner);
-                if (corner) cq[cn + __popcll(m & below)] = (uint16_t)(((rt + 1) << 9) | (cb + j + 1));
+                if (corner) cq[cn + __popcll(m & below)] = c;
                 cn += __popcll(m);
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
