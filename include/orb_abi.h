@@ -100,6 +100,17 @@ int orb_extract_batch_device(orb_extractor_t* h, int B, const uint8_t* d_imgs, i
 int orb_extract_batch(orb_extractor_t* h, int B, const uint8_t* imgs, int w, int hgt, int stride,
                       int64_t frame_pitch, orb_keypoint_t* kps_out, uint8_t* desc_out, int32_t* n_out);
 
+/* Colour frames: Tracking::GrabImage's cvtColor(image, im, mbRGB ? CV_RGB2GRAY : CV_BGR2GRAY)
+ * (reference Tracking.cc:202-207; OpenCV 2.4 fixed-point luma, exact) fused into the level-0
+ * pass, then the same extraction.  channels 3 or 4 (interleaved u8, row pitch `stride` bytes >=
+ * w * channels); rgb != 0 for RGB channel order, 0 for BGR.  Otherwise as orb_extract_batch_device
+ * / orb_extract. */
+int orb_extract_batch_device_color(orb_extractor_t* h, int B, const uint8_t* d_imgs, int w, int hgt, int stride,
+                                   int64_t frame_pitch, int channels, int rgb, orb_keypoint_t* d_kps, uint8_t* d_desc,
+                                   int32_t* d_counts, void* stream);
+int orb_extract_color(orb_extractor_t* h, const uint8_t* img, int w, int hgt, int stride, int channels, int rgb,
+                      orb_keypoint_t* kps_out, int kps_cap, uint8_t* desc_out, int* n_out);
+
 /* ---- ORBmatcher -------------------------------------------------------------------- */
 /* ORBmatcher::DescriptorDistance (reference ORBmatcher.cc:1794-1810; DBoW2 FORB.cpp:81-101). */
 int orb_descriptor_distance(const uint8_t* a, const uint8_t* b);
@@ -377,6 +388,8 @@ const char* orb_profile_stage_name(int i);
 /* Host instantiation of the kernels' libstdc++ nth_element replay on packed u32 elements
  * (score in bits 24..31), for CPU unit tests against std::nth_element. */
 int orb_debug_nth_element_u32(uint32_t* a, int n, int nth);
+/* The one-wave (ballot-partition) replay k_select uses, run on `device` (n <= 8192). */
+int orb_debug_nth_element_wave_u32(uint32_t* a, int n, int nth, int device);
 /* Padded pyramid level l of batch frame b after the last extraction (device sync). */
 int orb_debug_level_image(orb_extractor_t* h, int b, int l, uint8_t* out, int* w, int* hgt);
 /* Descriptor image (blurred ROI + un-blurred padding ring) of level l, frame b, padded

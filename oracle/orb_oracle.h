@@ -120,6 +120,9 @@ int oracle_search_for_triangulation(const orb_frame_view_t* KF1, const uint8_t* 
                                     const float* F12, float nnratio, int check_ori, int32_t* match12,
                                     int* n_matches);
 
+/* ---- orb_oracle_color.cpp: cvtColor(CV_RGB2GRAY / CV_BGR2GRAY) 8U (Tracking.cc:202-207) ---- */
+int oracle_rgb_to_gray(const uint8_t* src, int w, int h, int stride, int cn, int rgb, uint8_t* dst);
+
 /* ---- orb_oracle_mappoint.cpp: MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:185-250) */
 int oracle_compute_distinctive_descriptors(int M, const int32_t* offsets, const uint8_t* desc, const uint8_t* usable,
                                            int32_t* best_row, uint8_t* out_desc);

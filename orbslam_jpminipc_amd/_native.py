@@ -113,6 +113,8 @@ HIP_SIGNATURES = {
     "orb_extract": (_i, [_vp, _vp, _i, _i, _i, _vp, _i, _vp, ctypes.POINTER(_i)]),
     "orb_extract_batch_device": (_i, [_vp, _i, _vp, _i, _i, _i, _i64, _vp, _vp, _vp, _vp]),
     "orb_extract_batch": (_i, [_vp, _i, _vp, _i, _i, _i, _i64, _vp, _vp, _vp]),
+    "orb_extract_batch_device_color": (_i, [_vp, _i, _vp, _i, _i, _i, _i64, _i, _i, _vp, _vp, _vp, _vp]),
+    "orb_extract_color": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _i, _vp, ctypes.POINTER(_i)]),
     "orb_descriptor_distance": (_i, [_vp, _vp]),
     "orb_search_for_initialization": (
         _i,
@@ -164,6 +166,7 @@ HIP_SIGNATURES = {
     "orb_profile_read": (_i, [_vp, _vp, _vp, _i]),
     "orb_profile_stage_name": (ctypes.c_char_p, [_i]),
     "orb_debug_nth_element_u32": (_i, [_vp, _i, _i]),
+    "orb_debug_nth_element_wave_u32": (_i, [_vp, _i, _i, _i]),
     "orb_debug_level_image": (_i, [_vp, _i, _i, _vp, ctypes.POINTER(_i), ctypes.POINTER(_i)]),
     "orb_debug_cell_counts": (_i, [_vp, _i, _i, _vp, _i]),
     "orb_debug_blur_image": (_i, [_vp, _i, _i, _vp]),

@@ -176,6 +176,94 @@ ORB_HD inline int retain_best(T* a, int n, int keep, Greater comp) {
     return keep;
 }
 
+#if defined(__HIPCC__)
+// The same permutation computed by one wave (array and scratch in LDS).  libstdc++'s
+// __unguarded_partition(lo, hi, pivot) advances a left cursor over elements comp(x, pivot) and
+// a right cursor over comp(pivot, x), swapping where both stop.  Its k-th swap therefore
+// exchanges L_k (the k-th left stopper from the left: !comp(a[p], pivot)) with R_k (the k-th
+// right stopper from the right: !comp(pivot, a[p]); the pivot slot lo-1 is the last one) for
+// as long as L_k < R_k, and it returns L_K when that lies below R_{K-1}, else R_{K-1} (the left
+// cursor stops on the element the previous swap put there).  Positions in the untouched middle
+// keep their original values, so the stopper lists of the original array decide everything:
+// ballot-compacted lists, a ballot count of K, disjoint swaps.
+template <class T, class Greater>
+__device__ inline int unguarded_partition_wave(T* a, int lo, int hi, T pv, Greater comp, uint16_t* Lp, uint16_t* Rp,
+                                               int lane) {
+    const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+    int nl = 0, nr = 0;
+    for (int c0 = lo; c0 < hi; c0 += 64) {
+        const int p = c0 + lane;
+        bool ls = false, rs = false;
+        if (p < hi) {
+            const T v = a[p];
+            ls = !comp(v, pv);
+            rs = !comp(pv, v);
+        }
+        const uint64_t mL = __ballot(ls), mR = __ballot(rs);
+        if (ls) Lp[nl + __popcll(mL & below)] = (uint16_t)p;
+        if (rs) Rp[nr + __popcll(mR & below)] = (uint16_t)p;
+        nl += __popcll(mL);
+        nr += __popcll(mR);
+    }
+    // R_k = Rp[nr - 1 - k] (k < nr), R_nr = lo - 1; L_k < R_k holds for a prefix k < K
+    int K = 0;
+    for (int k0 = 0; k0 < nl; k0 += 64) {
+        const int k = k0 + lane;
+        bool ok = false;
+        if (k < nl) ok = (int)Lp[k] < (k < nr ? (int)Rp[nr - 1 - k] : lo - 1);
+        const uint64_t m = __ballot(ok);
+        K += __popcll(m);
+        if (m != ~0ull) break;
+    }
+    for (int k = lane; k < K; k += 64) {
+        const int l = Lp[k], r = k < nr ? (int)Rp[nr - 1 - k] : lo - 1;
+        const T x = a[l], y = a[r];
+        a[l] = y;
+        a[r] = x;
+    }
+    const int LK = K < nl ? (int)Lp[K] : 0x7fffffff;
+    const int Rprev = K == 0 ? hi : (K - 1 < nr ? (int)Rp[nr - K] : lo - 1);
+    return LK < Rprev ? LK : Rprev;
+}
+
+// std::nth_element(a, a + nth, a + n, comp) by one wave of a workgroup (a, Lp, Rp in LDS;
+// Lp / Rp hold n u16 each).  The median-of-3, the depth-limited heap fallback and the final
+// insertion sort are the sequential code on lane 0; LDS accesses of one wave complete in
+// order, so every lane sees lane 0's writes.
+template <class T, class Greater>
+__device__ inline void nth_element_wave(T* a, int nth, int n, Greater comp, uint16_t* Lp, uint16_t* Rp, int lane) {
+    if (n == 0 || nth == n) return;
+    int first = 0, last = n, depth = lg(n) * 2;
+    while (last - first > 3) {
+        if (depth == 0) {
+            if (lane == 0) {
+                heap_select(a, first, nth + 1, last, comp);
+                swap_at(a, first, nth);
+            }
+            return;
+        }
+        --depth;
+        const int mid = first + (last - first) / 2;
+        if (lane == 0) move_median_to_first(a, first, first + 1, mid, last - 1, comp);
+        const T pv = a[first];
+        const int cut = unguarded_partition_wave(a, first + 1, last, pv, comp, Lp, Rp, lane);
+        if (cut <= nth)
+            first = cut;
+        else
+            last = cut;
+    }
+    if (lane == 0) insertion_sort(a, first, last, comp);
+}
+
+template <class T, class Greater>
+__device__ inline int retain_best_wave(T* a, int n, int keep, Greater comp, uint16_t* Lp, uint16_t* Rp, int lane) {
+    if (n <= keep) return n;
+    if (keep <= 0) return 0;
+    nth_element_wave(a, keep, n, comp, Lp, Rp, lane);
+    return keep;
+}
+#endif
+
 }  // namespace orbsel
 
 #endif

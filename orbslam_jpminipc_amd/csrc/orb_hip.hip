@@ -45,7 +45,17 @@
 #endif
 #ifndef KL_SKIP_QUEUE
 #define KL_SKIP_QUEUE 0
-#endif  // level list kept in LDS when it fits (u32 entries)
+#endif
+// k_select ablations (timing-only, likewise): FAST(7) re-run, per-cell and per-level retainBest
+#ifndef KS_SKIP_RERUN
+#define KS_SKIP_RERUN 0
+#endif
+#ifndef KS_SKIP_RETAIN
+#define KS_SKIP_RETAIN 0
+#endif
+#ifndef KS_SKIP_LEVEL_RETAIN
+#define KS_SKIP_LEVEL_RETAIN 0
+#endif
 
 // ======================================================================================
 // error plumbing
@@ -132,6 +142,31 @@ __global__ void __launch_bounds__(256) k_pyr0(const uint8_t* __restrict__ imgs, 
         int px = x4 + i;
         uint32_t v = 0;
         if (px < lg.w + 2 * EDGE) v = src[reflect101(px - EDGE, lg.w)];
+        word |= v << (8 * i);
+    }
+    *(uint32_t*)(pyr + lg.base + (long long)b * lg.fstride + (long long)py * lg.pitch + x4) = word;
+}
+
+// Level 0 from 3- or 4-channel frames: Tracking::GrabImage's cvtColor(.., CV_RGB2GRAY /
+// CV_BGR2GRAY) (Tracking.cc:202-207) fused with the padding.  OpenCV 2.4's RGB2Gray<uchar> is an
+// exact fixed-point sum, (c0*p[0] + 9617*p[1] + c2*p[2] + 2^13) >> 14 with R2Y = 4899,
+// G2Y = 9617, B2Y = 1868 (yuv_shift 14): (c0, c2) = (R2Y, B2Y) for RGB order, (B2Y, R2Y) for BGR.
+__global__ void __launch_bounds__(256) k_pyr0_color(const uint8_t* __restrict__ imgs, int stride, long long fpitch,
+                                                    int cn, int c0, int c2, uint8_t* __restrict__ pyr, Geom g) {
+    const LevelGeom& lg = g.lv[0];
+    const int b = blockIdx.z, py = blockIdx.y * 4 + threadIdx.y;
+    const int x4 = (blockIdx.x * 64 + threadIdx.x) * 4;
+    if (x4 >= lg.pitch || py >= lg.ph) return;
+    const uint8_t* src = imgs + (long long)b * fpitch + (long long)reflect101(py - EDGE, lg.h) * stride;
+    uint32_t word = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int px = x4 + i;
+        uint32_t v = 0;
+        if (px < lg.w + 2 * EDGE) {
+            const uint8_t* p = src + (long long)reflect101(px - EDGE, lg.w) * cn;
+            v = (uint32_t)((c0 * p[0] + 9617 * p[1] + c2 * p[2] + (1 << 13)) >> 14);
+        }
         word |= v << (8 * i);
     }
     *(uint32_t*)(pyr + lg.base + (long long)b * lg.fstride + (long long)py * lg.pitch + x4) = word;
@@ -564,7 +599,7 @@ __global__ void __launch_bounds__(256) k_select(const uint8_t* __restrict__ pyr,
     // (1) FAST(cellImage, keys, 7, true) where a cell kept <= 3 (a skipped cell is `continue`d)
     {
         const int nfb = s_fb[ORB_MAX_CELLS_PER_LEVEL];
-        for (int f = 0; f < nfb; ++f) {
+        for (int f = 0; f < (KS_SKIP_RERUN ? 0 : nfb); ++f) {
             const int c = s_fb[f];
             const CellGeom cg = lc[c];
             const int dw = cg.hx - 6, dh = cg.hy - 6;
@@ -711,7 +746,7 @@ __global__ void __launch_bounds__(256) k_select(const uint8_t* __restrict__ pyr,
     ScoreGreater comp;
     for (int c = tid; c < nC; c += 256) {
         uint32_t* seg = srt + (inLds ? s_off[c] : lc[c].candOff);
-        s_cnt[c] = orbsel::retain_best(seg, s_cnt[c], s_ret[c], comp);
+        s_cnt[c] = KS_SKIP_RETAIN ? min(s_cnt[c], max(s_ret[c], 0)) : orbsel::retain_best(seg, s_cnt[c], s_ret[c], comp);
     }
     __syncthreads();
     if (tid == 0) {
@@ -741,7 +776,13 @@ __global__ void __launch_bounds__(256) k_select(const uint8_t* __restrict__ pyr,
     int keep = K;
     if (K > lg.nDesired) {
         keep = lg.nDesired;
-        if (tid == 0) orbsel::retain_best(list, K, lg.nDesired, comp);
+        if (inLds) {  // one wave, partitions by ballot (nth_select.h); scratch = the free srt region
+            uint16_t* Lp = (uint16_t*)srt;
+            if (wave == 0 && !KS_SKIP_LEVEL_RETAIN)
+                orbsel::retain_best_wave(list, K, lg.nDesired, comp, Lp, Lp + K, lane);
+        } else if (tid == 0 && !KS_SKIP_LEVEL_RETAIN) {
+            orbsel::retain_best(list, K, lg.nDesired, comp);
+        }
     }
     __syncthreads();
     uint32_t* out = lvlOut + (long long)b * g.kpCap + lg.kpBase;
@@ -758,8 +799,10 @@ __global__ void __launch_bounds__(256) k_select(const uint8_t* __restrict__ pyr,
 // T = sum_j k_j sum_i k_i P; columns x < 4*floor(w/4) round T/65536 half-to-even (the SSE2
 // SymmColumnVec_32s8u float path), the tail columns half-up ((T + 2^15) >> 16).
 #define BLUR_TW 256  // output columns per tile: 64 lanes x 4 pixels
-#define BLUR_RW 16   // output rows per wave
-#define BLUR_TH 64   // output rows per tile (4 waves)
+#ifndef BLUR_RW
+#define BLUR_RW 12   // output rows per wave (48-row tiles: ~39 KB LDS, 4 work-groups per CU)
+#endif
+#define BLUR_TH (4 * BLUR_RW)  // output rows per tile (4 waves)
 #define BLUR_IW 66   // LDS row pitch in dwords: tile columns x0-4 .. x0+259
 struct BlurTile {
     int level, x0, y0;  // tile origin in level coordinates: x0 = -4 + 256 k, y0 = -3 + 64 m
@@ -787,7 +830,7 @@ typedef short i16x2 __attribute__((ext_vector_type(2)));
 // fits, so the queue is drained once, after the row loop.  u16 entry = rowCode << 11 |
 // laneCode << 4 | mask: tile row = wave*BLUR_RW - 1 + rowCode (0..17), bit j of mask is tile
 // column 4*(laneCode-1) + j (laneCode 0 and 65 carry the halo columns -1 and 256).
-#define LVL_FQ (18 * 64 + 2 * 18)
+#define LVL_FQ ((BLUR_RW + 2) * 64 + 2 * (BLUR_RW + 2))
 #define LVL_CQ 256   // per-wave corner / survivor chunk (u16 entries)
 #define LVL_SPW 264  // LDS strength-plane row pitch (bytes): tile columns -4 .. 259
 
@@ -1101,8 +1144,13 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
                                                      const float* __restrict__ lvlResp) {
     __shared__ __attribute__((aligned(16))) uint32_t s_patch[4][31 * IC_P / 4];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int b = blockIdx.y;
-    const int k = blockIdx.x * 4 + wave;
+    // XCD-aware block order: workgroup i runs on XCD i % 8, so give each XCD a contiguous run
+    // of keypoints (neighbouring keypoints share patch rows: L2 hits instead of HBM re-reads)
+    int bid = blockIdx.y * gridDim.x + blockIdx.x;
+    const int full = (gridDim.x * gridDim.y) & ~7;
+    if (bid < full) bid = (bid & 7) * (full >> 3) + (bid >> 3);
+    const int b = bid / gridDim.x;
+    const int k = (bid - b * gridDim.x) * 4 + wave;
     // locate the level of keypoint k (level-major output order, ORBextractor.cc:749-778)
     int l = -1, total = 0, idx = 0;
     for (int i = 0; i < g.L; ++i) {
@@ -1928,7 +1976,7 @@ struct orb_extractor {
     }
 
     int launch(int B, const uint8_t* d_imgs, int stride, long long fpitch, orb_keypoint_t* kps, uint8_t* desc,
-               int* counts, hipStream_t st) {
+               int* counts, hipStream_t st, int cn = 1, int rgb = 0) {
         if (prof && evNext > 4096) {  // bound the pool between reads
             int r = profile_collect();
             if (r) return r;
@@ -1937,7 +1985,11 @@ struct orb_extractor {
         {
             const LevelGeom& lg = g.lv[0];
             dim3 grid((lg.pitch / 4 + 63) / 64, (lg.ph + 3) / 4, B);
-            hipLaunchKernelGGL(k_pyr0, grid, dim3(64, 4), 0, st, d_imgs, stride, fpitch, d_pyr, g);
+            if (cn == 1)
+                hipLaunchKernelGGL(k_pyr0, grid, dim3(64, 4), 0, st, d_imgs, stride, fpitch, d_pyr, g);
+            else  // R2Y on the red channel, B2Y on the blue one
+                hipLaunchKernelGGL(k_pyr0_color, grid, dim3(64, 4), 0, st, d_imgs, stride, fpitch, cn,
+                                   rgb ? 4899 : 1868, rgb ? 1868 : 4899, d_pyr, g);
         }
         stage_end(st);
         stage_begin(1, st);
@@ -2122,6 +2174,65 @@ int orb_extract(orb_extractor_t* h, const uint8_t* img, int w, int hgt, int stri
     return ORB_OK;
 }
 
+int orb_extract_batch_device_color(orb_extractor_t* h, int B, const uint8_t* d_imgs, int w, int hgt, int stride,
+                                   int64_t frame_pitch, int channels, int rgb, orb_keypoint_t* d_kps, uint8_t* d_desc,
+                                   int32_t* d_counts, void* stream) {
+    if (!h || B <= 0 || !d_imgs || !d_kps || !d_desc || !d_counts) return set_err(ORB_EINVAL, "bad arguments");
+    if (channels != 3 && channels != 4) return set_err(ORB_EINVAL, "channels must be 3 or 4");
+    if (B > h->maxBatch) return set_err(ORB_EINVAL, "B exceeds max_batch");
+    if (w <= 0 || hgt <= 0 || stride < w * channels || frame_pitch < (int64_t)stride * hgt)
+        return set_err(ORB_EINVAL, "bad image geometry");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;
+    if (w != h->W || hgt != h->H) {
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        HIP_TRY(hipStreamSynchronize(h->lastStream));
+        int r = h->build_geometry(w, hgt);
+        if (r) return r;
+    }
+    h->lastStream = st;
+    return h->launch(B, d_imgs, stride, frame_pitch, d_kps, d_desc, d_counts, st, channels, rgb);
+}
+
+int orb_extract_color(orb_extractor_t* h, const uint8_t* img, int w, int hgt, int stride, int channels, int rgb,
+                      orb_keypoint_t* kps_out, int kps_cap, uint8_t* desc_out, int* n_out) {
+    if (!h || !n_out) return set_err(ORB_EINVAL, "bad arguments");
+    if (w <= 0 || hgt <= 0) {  // _image.empty(): return, outputs untouched (ORBextractor.cc:721-722)
+        *n_out = 0;
+        return ORB_OK;
+    }
+    if (!img || !kps_out || !desc_out) return set_err(ORB_EINVAL, "bad arguments");
+    if (channels != 3 && channels != 4) return set_err(ORB_EINVAL, "channels must be 3 or 4");
+    if (stride < w * channels) return set_err(ORB_EINVAL, "bad image geometry");
+    HIP_TRY(hipSetDevice(h->device));
+    if (w != h->W || hgt != h->H) {
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        HIP_TRY(hipStreamSynchronize(h->lastStream));
+        int r = h->build_geometry(w, hgt);
+        if (r) return r;
+    }
+    int st = h->ensure_staging();
+    if (st) return st;
+    const size_t row = (size_t)w * channels;
+    uint8_t* dimg = nullptr;
+    HIP_TRY(hipMalloc(&dimg, row * hgt));
+    hipError_t e = hipMemcpy2DAsync(dimg, row, img, stride, row, (size_t)hgt, hipMemcpyHostToDevice, h->stream);
+    int32_t n = 0;
+    if (e == hipSuccess)
+        st = h->launch(1, dimg, (int)row, (long long)(row * hgt), h->d_kps, h->d_desc, h->d_counts, h->stream, channels,
+                       rgb);
+    if (e == hipSuccess && !st) e = hipMemcpyAsync(&n, h->d_counts, 4, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess && !st) e = hipStreamSynchronize(h->stream);
+    (void)hipFree(dimg);
+    if (st) return st;
+    if (e != hipSuccess) return set_err(ORB_EDEVICE, std::string("colour extraction: ") + hipGetErrorString(e));
+    if (n > kps_cap) return set_err(ORB_ERANGE, "kps_cap smaller than the number of keypoints");
+    HIP_TRY(hipMemcpy(kps_out, h->d_kps, (size_t)n * sizeof(orb_keypoint_t), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(desc_out, h->d_desc, (size_t)n * 32, hipMemcpyDeviceToHost));
+    *n_out = n;
+    return ORB_OK;
+}
+
 int orb_descriptor_distance(const uint8_t* a, const uint8_t* b) {
     int dist = 0;
     for (int i = 0; i < 8; ++i) {
@@ -2261,6 +2372,39 @@ const char* orb_profile_stage_name(int i) {
 int orb_debug_nth_element_u32(uint32_t* a, int n, int nth) {
     ScoreGreater comp;
     orbsel::nth_element(a, nth, n, comp);
+    return ORB_OK;
+}
+
+}  // extern "C"
+
+__global__ void __launch_bounds__(64) k_debug_nth_wave(uint32_t* a, int n, int nth) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_a[];
+    uint16_t* Lp = (uint16_t*)(s_a + n);
+    for (int i = threadIdx.x; i < n; i += 64) s_a[i] = a[i];
+    __syncthreads();
+    ScoreGreater comp;
+    orbsel::nth_element_wave(s_a, nth, n, comp, Lp, Lp + n, (int)threadIdx.x);
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += 64) a[i] = s_a[i];
+}
+
+extern "C" {
+
+int orb_debug_nth_element_wave_u32(uint32_t* a, int n, int nth, int device) {
+    if (!a || n < 0 || n > 8192 || nth < 0 || nth > n) return set_err(ORB_EINVAL, "bad arguments");
+    if (n == 0) return ORB_OK;
+    HIP_TRY(hipSetDevice(device));
+    uint32_t* d = nullptr;
+    HIP_TRY(hipMalloc(&d, (size_t)n * 4));
+    hipError_t e = hipMemcpy(d, a, (size_t)n * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        (void)hipFuncSetAttribute((const void*)k_debug_nth_wave, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
+        hipLaunchKernelGGL(k_debug_nth_wave, dim3(1), dim3(64), (size_t)n * 8, 0, d, n, nth);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(a, d, (size_t)n * 4, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return set_err(ORB_EDEVICE, std::string("nth_element_wave: ") + hipGetErrorString(e));
     return ORB_OK;
 }
 

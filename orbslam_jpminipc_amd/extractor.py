@@ -123,6 +123,45 @@ class ORBextractor:
         return d_kps, d_desc, d_counts
 
 
+    # ---- colour frames: Tracking::GrabImage's cvtColor fused with level 0 (Tracking.cc:202-207)
+    def extract_color(self, image, rgb: bool = True):
+        """operator() on cvtColor(image, mbRGB ? CV_RGB2GRAY : CV_BGR2GRAY); image (H, W, 3|4) uint8."""
+        img = np.asarray(image)
+        if img.size == 0:
+            return None, None
+        if img.dtype != np.uint8 or img.ndim != 3 or img.shape[2] not in (3, 4):
+            raise TypeError("image must be an (H, W, 3|4) uint8 array")
+        img = np.ascontiguousarray(img)
+        h, w, cn = img.shape
+        cap = self.max_keypoints
+        kps = np.empty(cap, KEYPOINT_DTYPE)
+        desc = np.empty((cap, 32), np.uint8)
+        n = ctypes.c_int()
+        check(self._lib.orb_extract_color(self._h, ptr(img), w, h, w * cn, cn, int(bool(rgb)), ptr(kps), cap, ptr(desc),
+                                          ctypes.byref(n)))
+        n = n.value
+        return kps[:n].copy(), (desc[:n].copy() if n > 0 else None)
+
+    def extract_batch_device_color(self, d_imgs, rgb: bool = True, d_kps=None, d_desc=None, d_counts=None,
+                                   stream=None):
+        """extract_batch_device on (B, H, W, 3|4) uint8 device frames, converted to gray on the fly."""
+        import torch
+
+        B, h, w, cn = d_imgs.shape
+        cap = self.max_keypoints
+        dev = d_imgs.device
+        if d_kps is None:
+            d_kps = torch.empty((B, cap, 28), dtype=torch.uint8, device=dev)
+        if d_desc is None:
+            d_desc = torch.empty((B, cap, 32), dtype=torch.uint8, device=dev)
+        if d_counts is None:
+            d_counts = torch.empty((B,), dtype=torch.int32, device=dev)
+        s = stream if stream is not None else torch.cuda.current_stream(dev)
+        check(self._lib.orb_extract_batch_device_color(self._h, B, ptr(d_imgs), w, h, d_imgs.stride(1),
+                                                       d_imgs.stride(0), cn, int(bool(rgb)), ptr(d_kps), ptr(d_desc),
+                                                       ptr(d_counts), ctypes.c_void_p(s.cuda_stream)))
+        return d_kps, d_desc, d_counts
+
     # ---- measurement ----------------------------------------------------------------------
     def profile_enable(self, enable: bool = True) -> None:
         """Record a HIP-event pair around every kernel stage of extract_batch_device."""
