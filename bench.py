@@ -65,6 +65,22 @@ def stage_bytes(W, H, n_kp, n_cand, n_pairs_kp0, B):
     }
 
 
+def pmc_traffic(kernel, W, H, B, NF):
+    """HBM bytes per launch of `kernel` from the committed PMC summary of this workload
+    (profiles/pmc_latest.json, written by scripts/pmc_summary.py from rocprofv3 FETCH_SIZE /
+    WRITE_SIZE passes over bench.py), or (None, None) when it does not cover this run."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_latest.json")) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    w = d.get("workload", {})
+    if (w.get("width"), w.get("height"), w.get("batch"), w.get("nfeatures")) != (W, H, B, NF):
+        return None, None
+    k = d.get("per_launch", {}).get(kernel)
+    return (k["hbm_bytes"], d.get("source")) if k else (None, None)
+
+
 def cpu_baseline(frames, nfeatures, threads, W, H):
     """Oracle (test infrastructure, oracle/liborb_oracle.so) on a bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -94,7 +110,8 @@ def main():
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--nfeatures", type=int, default=1000)
-    ap.add_argument("--cpu-frames", type=int, default=1024, help="CPU-baseline sample size (0 = skip)")
+    ap.add_argument("--cpu-frames", type=int, default=3072,
+                    help="CPU-baseline sample size (0 = skip); ~20 s of CPU-thread time on 16 threads")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = OMP_NUM_THREADS or os.cpu_count()")
     args = ap.parse_args()
 
@@ -204,6 +221,7 @@ def main():
     per_step_s = tmax / args.steps
 
     value = replicas.whole_job_rate(B * args.steps, world, tmax)
+    traffic, traffic_src = pmc_traffic(dom, W, H, B, NF)
     result = {
         "metric": "frames/sec ORB extract+match, 640x480 8-level 1000 kp; HBM GB/s vs peak",
         "value": value,
@@ -231,7 +249,10 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": ds["GBps"] / HBM_PEAK_GBS if ds["GBps"] else None,
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_unit": "bytes per launch (rocprofv3 PMC)",
+            "traffic_source": traffic_src,
+            "algorithmic_bytes_per_launch": ds["bytes_per_launch"],
         },
         "pipeline": {
             "algorithmic_bytes_per_step": b_ext + b_match,

@@ -36,7 +36,8 @@ def main():
             if not k.startswith("__amd") and "elementwise" not in k and "at::" not in k}
     known = a.batch * a.width * a.height
     cal = known / (mean["k_pyr0"]["FETCH_SIZE"] * 1024.0) if "k_pyr0" in mean else None
-    out = {"workload": {"width": a.width, "height": a.height, "batch": a.batch, "nfeatures": a.nfeatures},
+    out = {"source": a.root.rstrip("/").split("/")[-1],
+           "workload": {"width": a.width, "height": a.height, "batch": a.batch, "nfeatures": a.nfeatures},
            "read_calibration": {"kernel": "k_pyr0", "known_read_bytes": known, "factor": cal},
            "per_launch": {}}
     for k, d in sorted(mean.items()):
