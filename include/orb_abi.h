@@ -381,6 +381,9 @@ int orb_vocabulary_transform(orb_vocabulary_t* v, const uint8_t* desc, int n, in
  * stage (stage names via orb_profile_stage_name); the return value is the stage count.
  * Enabling (or re-enabling) resets the counters. */
 int orb_profile_enable(orb_extractor_t* h, int enable);
+/* The same for a subset of stages (bit k = stage k): every event pair is a stream boundary
+ * (≈10 µs measured), so a timed run brackets only the stage it reports. */
+int orb_profile_enable_stages(orb_extractor_t* h, unsigned stage_mask);
 int orb_profile_read(orb_extractor_t* h, double* stage_ms, int64_t* stage_launches, int nstages);
 const char* orb_profile_stage_name(int i);
 

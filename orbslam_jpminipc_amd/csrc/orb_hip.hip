@@ -128,23 +128,53 @@ using namespace orbdev;
 __constant__ signed char c_pattern[1024];
 
 // ---- pyramid --------------------------------------------------------------------------
-// Level 0: copyMakeBorder(image, 16, BORDER_REFLECT_101); one thread per 4 output bytes.
+// Level 0: copyMakeBorder(image, 16, BORDER_REFLECT_101); one thread per 16-byte chunk of a
+// padded row (pitch is a multiple of 16).  Interior chunks (source columns [x-16, x) inside the
+// row) are one 16-, four 4- or sixteen 1-byte loads depending on the source alignment and one
+// 16-byte store; the two border chunks per side reflect byte by byte.
 __global__ void __launch_bounds__(256) k_pyr0(const uint8_t* __restrict__ imgs, int stride, long long fpitch,
                                               uint8_t* __restrict__ pyr, Geom g) {
     const LevelGeom& lg = g.lv[0];
-    const int b = blockIdx.z, py = blockIdx.y * 4 + threadIdx.y;
-    const int x4 = (blockIdx.x * 64 + threadIdx.x) * 4;
-    if (x4 >= lg.pitch || py >= lg.ph) return;
+    const int nchunk = lg.pitch >> 4;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int py = i / nchunk, x16 = (i - py * nchunk) << 4;
+    if (py >= lg.ph) return;
+    const int b = blockIdx.y;
     const uint8_t* src = imgs + (long long)b * fpitch + (long long)reflect101(py - EDGE, lg.h) * stride;
-    uint32_t word = 0;
+    uint4 out;
+    if (x16 >= EDGE && x16 <= lg.w) {
+        const uint8_t* p = src + (x16 - EDGE);
+        const uintptr_t a = (uintptr_t)p;
+        if ((a & 15u) == 0) {
+            out = *(const uint4*)p;
+        } else if ((a & 3u) == 0) {
+            const uint32_t* q = (const uint32_t*)p;
+            out = make_uint4(q[0], q[1], q[2], q[3]);
+        } else {
+            uint32_t w[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        int px = x4 + i;
-        uint32_t v = 0;
-        if (px < lg.w + 2 * EDGE) v = src[reflect101(px - EDGE, lg.w)];
-        word |= v << (8 * i);
+            for (int k = 0; k < 4; ++k)
+                w[k] = (uint32_t)p[4 * k] | ((uint32_t)p[4 * k + 1] << 8) | ((uint32_t)p[4 * k + 2] << 16) |
+                       ((uint32_t)p[4 * k + 3] << 24);
+            out = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+    } else {
+        uint32_t w[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint32_t word = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int px = x16 + 4 * k + j;
+                uint32_t v = 0;
+                if (px < lg.w + 2 * EDGE) v = src[reflect101(px - EDGE, lg.w)];
+                word |= v << (8 * j);
+            }
+            w[k] = word;
+        }
+        out = make_uint4(w[0], w[1], w[2], w[3]);
     }
-    *(uint32_t*)(pyr + lg.base + (long long)b * lg.fstride + (long long)py * lg.pitch + x4) = word;
+    *(uint4*)(pyr + lg.base + (long long)b * lg.fstride + (long long)py * lg.pitch + x16) = out;
 }
 
 // Level 0 from 3- or 4-channel frames: Tracking::GrabImage's cvtColor(.., CV_RGB2GRAY /
@@ -172,28 +202,32 @@ __global__ void __launch_bounds__(256) k_pyr0_color(const uint8_t* __restrict__ 
     *(uint32_t*)(pyr + lg.base + (long long)b * lg.fstride + (long long)py * lg.pitch + x4) = word;
 }
 
-// Copy `rows` rows of `words` dwords (global row stride gsw words, LDS row stride lsw words)
-// with 256 threads: waves take rows, lanes take words, and every thread issues up to 8
-// independent loads before its LDS stores (k_pyr_resize's narrow, tall source tiles).
-__device__ __forceinline__ void stage_rows_by_wave(uint32_t* __restrict__ dst, int lsw,
-                                                   const uint32_t* __restrict__ src, long long gsw, int rows,
-                                                   int words, int wave, int lane) {
-    for (int wx0 = 0; wx0 < words; wx0 += 64) {
-        const int wx = wx0 + lane;
-        const bool colok = wx < words;
-        for (int r0 = wave; r0 < rows; r0 += 32) {
-            uint32_t v[8];
+// Stage `rows` x `units` 16-byte units (global row pitch gsu units, LDS row pitch the same
+// `units`) with 256 threads, up to RZ_SB units per thread all in flight before any LDS write:
+// a k_pyr_resize source tile is one memory round trip.
+#define RZ_SB 8
+__device__ __forceinline__ void stage_tile16(uint4* __restrict__ dst, const uint4* __restrict__ src, long long gsu,
+                                             int rows, int units, int tid) {
+    const int total = rows * units;
+    const int dr = 256 / units, dc = 256 - dr * units;
+    for (int base = 0; base < total; base += RZ_SB * 256) {
+        const int i0 = base + tid;
+        const int r0 = i0 / units, c0 = i0 - r0 * units;
+        uint4 v[RZ_SB];
+        int r = r0, c = c0;
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const int r = r0 + 4 * k;
-                v[k] = (colok && r < rows) ? src[(long long)r * gsw + wx] : 0u;
-            }
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const int r = r0 + 4 * k;
-                if (colok && r < rows) dst[r * lsw + wx] = v[k];
+        for (int k = 0; k < RZ_SB; ++k) {
+            if (i0 + k * 256 < total) v[k] = src[(long long)r * gsu + c];
+            r += dr;
+            c += dc;
+            if (c >= units) {
+                c -= units;
+                ++r;
             }
         }
+#pragma unroll
+        for (int k = 0; k < RZ_SB; ++k)
+            if (i0 + k * 256 < total) dst[i0 + k * 256] = v[k];
     }
 }
 
@@ -242,78 +276,125 @@ __device__ __forceinline__ void stage_rows_to_lds(uint32_t* __restrict__ dst, in
 // scalar FixedPtCast<int,uchar,22> tail; then copyMakeBorder(REFLECT_101 | ISOLATED), fused
 // by evaluating the resize at the reflected coordinate of every padded pixel.
 // One workgroup per RZ_TW x RZ_TH tile of the padded level: the source rectangle the tile
-// reads (host table: first dword column, dwords, first row, rows) is staged into LDS with
-// coalesced dword loads; a thread owns 4 padded columns (taps in registers) and walks the
-// RZ_TH / 4 rows of its wave, gathering the 2x2 taps from LDS.
+// reads (host table: first 16-byte column, 16-byte units, first row, rows) is staged into LDS
+// in one round trip of 16-byte loads; a thread owns 4 padded columns (taps in registers) and walks the
+// RZ_TH / 4 rows of its wave.  As in OpenCV, a source row's horizontal sums are computed once
+// and kept (two rows in registers) while consecutive output rows reuse them.
+// Every coefficient is in [0, 2050] with a0 + a1, b0 + b1 <= 2050 (checked on the host), so
+// no intermediate of the reference's saturating chain can saturate: H <= 255 * 2050 = 522750,
+// (H >> 4) * b < 2^27, the SSE2 sum <= 1023 and the scalar sum < 2^31; both end in [0, 255].
+// The SSE2 path's (h * b) >> 16 is then mulhi(h, b << 16).
 #define RZ_TW 256
-#define RZ_TH 32
+#define RZ_TH 64
 __global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, const int* __restrict__ rtab, Geom g,
                                                     int l) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_src[];
     const LevelGeom& lg = g.lv[l];
     const LevelGeom& ls = g.lv[l - 1];
-    const int b = blockIdx.z, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int b = blockIdx.z, tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int* tt = rtab + lg.rtile + 4 * (blockIdx.y * gridDim.x + blockIdx.x);
     const int colStart = tt[0], words = tt[1], rowMin = tt[2], nrows = tt[3];
     const uint8_t* S = pyr + ls.base + (long long)b * ls.fstride + (long long)EDGE * ls.pitch + EDGE;
-    stage_rows_by_wave(s_src, words, (const uint32_t*)(S + (long long)rowMin * ls.pitch + colStart), ls.pitch >> 2,
-                       nrows, words, wave, lane);
+    stage_tile16((uint4*)s_src, (const uint4*)(S + (long long)rowMin * ls.pitch + colStart), ls.pitch >> 4, nrows,
+                 words, tid);
     const int* xofs = rtab + lg.rtab;
     const int* alpha = xofs + lg.w;
     const int* yofs = alpha + lg.w;
     const int* beta = yofs + lg.h;
+    // the wave's RZ_TH / 4 row coefficients, one row per lane, fetched while the tile loads
+    // (read back with readlane: no dependent global load inside the row walk)
+    const int pyA = blockIdx.y * RZ_TH + wave * (RZ_TH / 4);
+    const int pyB = min(pyA + RZ_TH / 4, lg.ph);
+    int rowSy = 0, rowBeta = 0;
+    if (lane < RZ_TH / 4 && pyA + lane < pyB) {
+        const int ly = reflect101(pyA + lane - EDGE, lg.h);
+        rowSy = yofs[ly];
+        rowBeta = beta[ly];
+    }
     const int x4 = blockIdx.x * RZ_TW + 4 * lane;
-    int o0[4], o1[4], a0[4], a1[4];
-    bool live[4], simd[4];
+    uint32_t o0[4], o1[4], a0[4], a1[4];
+    uint32_t liveMask = 0;
+    bool allSimd = true;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int px = x4 + i;
-        live[i] = px < lg.w + 2 * EDGE;
+        if (px < lg.w + 2 * EDGE) liveMask |= 0xFFu << (8 * i);
         const int lx = reflect101(min(px, lg.w + 2 * EDGE - 1) - EDGE, lg.w);
         const int sx = xofs[lx];
         if (lx < lg.xmax) {
             const int aa = alpha[lx];
-            a0[i] = (short)(aa & 0xFFFF);
-            a1[i] = (short)(aa >> 16);
+            a0[i] = (uint32_t)(aa & 0xFFFF);
+            a1[i] = (uint32_t)(aa >> 16) & 0xFFFFu;
         } else {  // HResizeLinear tail: S[sx] * ONE (sx + 1 may be past the row: not read)
             a0[i] = 2048;
             a1[i] = 0;
         }
-        o0[i] = sx - colStart;
-        o1[i] = (a1[i] ? sx + 1 : sx) - colStart;
-        simd[i] = lx < lg.xs_resize;
+        o0[i] = (uint32_t)(sx - colStart);
+        o1[i] = (uint32_t)((a1[i] ? sx + 1 : sx) - colStart);
+        allSimd = allSimd && lx < lg.xs_resize;
     }
     __syncthreads();
     if (x4 >= lg.pitch) return;
     const uint8_t* L = (const uint8_t*)s_src;
-    const int LP = words * 4;
-    uint8_t* D = pyr + lg.base + (long long)b * lg.fstride + x4;
-    const int pyA = blockIdx.y * RZ_TH + wave * (RZ_TH / 4);
-    const int pyB = min(pyA + RZ_TH / 4, lg.ph);
-    for (int py = pyA; py < pyB; ++py) {
-        const int ly = reflect101(py - EDGE, lg.h);
-        const int sy = yofs[ly];
-        const int bb = beta[ly];
-        const int b0 = (short)(bb & 0xFFFF), b1 = (short)(bb >> 16);
-        const uint8_t* L0 = L + (min(max(sy, 0), ls.h - 1) - rowMin) * LP;
-        const uint8_t* L1 = L + (min(max(sy + 1, 0), ls.h - 1) - rowMin) * LP;
-        uint32_t word = 0;
+    const int LP = words * 16;
+    // horizontal sums of source row r: H >> 4 on the SSE2 columns, H on the scalar tail
+    auto hrow = [&](int r, uint32_t* h) {
+        const uint8_t* R = L + (r - rowMin) * LP;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int H0 = L0[o0[i]] * a0[i] + L0[o1[i]] * a1[i];
-            const int H1 = L1[o0[i]] * a0[i] + L1[o1[i]] * a1[i];
-            int r;
-            if (simd[i]) {
-                const int h0 = min(max(H0 >> 4, -32768), 32767), h1 = min(max(H1 >> 4, -32768), 32767);
-                int sm = min(max(((h0 * b0) >> 16) + ((h1 * b1) >> 16), -32768), 32767);
-                sm = min(max(sm + 2, -32768), 32767);
-                r = sm >> 2;
-            } else {
-                r = (H0 * b0 + H1 * b1 + (1 << 21)) >> 22;
-            }
-            word |= (live[i] ? (uint32_t)min(max(r, 0), 255) : 0u) << (8 * i);
+        for (int i = 0; i < 4; ++i) h[i] = (uint32_t)R[o0[i]] * a0[i] + (uint32_t)R[o1[i]] * a1[i];
+        if (allSimd) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) h[i] >>= 4;
         }
-        *(uint32_t*)(D + (long long)py * lg.pitch) = word;
+    };
+    uint8_t* D = pyr + lg.base + (long long)b * lg.fstride + x4;
+    int rA = -1, rB = -1;  // source rows held in hA / hB (wave-uniform)
+    uint32_t hA[4] = {0, 0, 0, 0}, hB[4] = {0, 0, 0, 0};
+    for (int py = pyA; py < pyB; ++py) {
+        const int sy = __builtin_amdgcn_readlane(rowSy, py - pyA);
+        const uint32_t bb = (uint32_t)__builtin_amdgcn_readlane(rowBeta, py - pyA);
+        const int s0 = min(max(sy, 0), ls.h - 1), s1 = min(max(sy + 1, 0), ls.h - 1);
+        if (s0 != rA) {
+            if (s0 == rB) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) hA[i] = hB[i];
+            } else {
+                hrow(s0, hA);
+            }
+            rA = s0;
+        }
+        if (s1 != rB) {
+            if (s1 == rA) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) hB[i] = hA[i];
+            } else {
+                hrow(s1, hB);
+            }
+            rB = s1;
+        }
+        const uint32_t b0 = bb & 0xFFFFu, b1 = bb >> 16;
+        uint32_t word;
+        if (allSimd) {
+            const uint32_t B0 = b0 << 16, B1 = b1 << 16;
+            uint32_t r[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) r[i] = (__umulhi(hA[i], B0) + __umulhi(hB[i], B1) + 2u) >> 2;
+            word = r[0] | (r[1] << 8) | (r[2] << 16) | (r[3] << 24);
+        } else {  // lanes holding a column of the scalar tail (hA / hB are full sums)
+            word = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int lx = reflect101(min(x4 + i, lg.w + 2 * EDGE - 1) - EDGE, lg.w);
+                uint32_t r;
+                if (lx < lg.xs_resize)
+                    r = (__umulhi(hA[i] >> 4, b0 << 16) + __umulhi(hB[i] >> 4, b1 << 16) + 2u) >> 2;
+                else
+                    r = (hA[i] * b0 + hB[i] * b1 + (1u << 21)) >> 22;
+                word |= r << (8 * i);
+            }
+        }
+        *(uint32_t*)(D + (long long)py * lg.pitch) = word & liveMask;
     }
 }
 
@@ -1132,9 +1213,14 @@ __global__ void __launch_bounds__(256) k_level(const uint8_t* __restrict__ pyr, 
 }
 
 // ---- orientation + descriptor -------------------------------------------------------------
-// One wave per keypoint.  IC angle on the raw level (31x31 disc staged in LDS with dword
-// loads); the 512 rBRIEF samples read the descriptor image built by k_level.
-#define IC_P 36  // LDS pitch of the 31-row IC patch
+// One wave per keypoint slot.  Two memory round trips per wave: (1) the slot's packed record
+// and the frame's per-level counts together; (2) the raw 31x31 IC patch and the 37x37 window
+// of the descriptor image that holds every rBRIEF sample (|offset| <= 18)
+// together, both into the wave's own LDS; the angle, sincos and the 512 samples then run
+// from LDS.  No workgroup barrier: a wave reads only what it wrote.
+#define IC_P 36   // LDS pitch of the 31-row IC patch (9 dwords used)
+#define DW_P 40   // LDS pitch of the 37-row descriptor window (10 dwords)
+#define DW_R 18   // window reach
 
 __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__ pyr,
                                                      const uint8_t* __restrict__ blur, Geom g,
@@ -1143,43 +1229,68 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
                                                      uint8_t* __restrict__ desc, int* __restrict__ counts,
                                                      const float* __restrict__ lvlResp) {
     __shared__ __attribute__((aligned(16))) uint32_t s_patch[4][31 * IC_P / 4];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __shared__ __attribute__((aligned(16))) uint32_t s_win[4][(2 * DW_R + 1) * DW_P / 4];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     // XCD-aware block order: workgroup i runs on XCD i % 8, so give each XCD a contiguous run
     // of keypoints (neighbouring keypoints share patch rows: L2 hits instead of HBM re-reads)
     int bid = blockIdx.y * gridDim.x + blockIdx.x;
     const int full = (gridDim.x * gridDim.y) & ~7;
     if (bid < full) bid = (bid & 7) * (full >> 3) + (bid >> 3);
     const int b = bid / gridDim.x;
-    const int k = (bid - b * gridDim.x) * 4 + wave;
-    // locate the level of keypoint k (level-major output order, ORBextractor.cc:749-778)
-    int l = -1, total = 0, idx = 0;
+    const int k = (bid - b * gridDim.x) * 4 + wave;  // slot: level l owns [kpBase_l, kpBase_l + nDesired_l)
+    int l = 0;
+    for (int i = 1; i < g.L; ++i)
+        if (k >= g.lv[i].kpBase) l = i;
+    const LevelGeom& lg = g.lv[l];
+    const int idx = k - lg.kpBase;
+    const uint32_t e = k < g.kpCap ? lvlOut[(long long)b * g.kpCap + k] : 0u;
+    // output position: level-major order (ORBextractor.cc:749-778)
+    int before = 0, cntL = 0, total = 0;
     for (int i = 0; i < g.L; ++i) {
-        const int cnt = lvlCount[(long long)b * g.L + i];
-        if (l < 0 && k < total + cnt) {
-            l = i;
-            idx = k - total;
-        }
-        total += cnt;
+        const int c = lvlCount[(long long)b * g.L + i];
+        before += i < l ? c : 0;
+        cntL = i == l ? c : cntL;
+        total += c;
     }
     if (k == 0 && lane == 0) counts[b] = total;
-    const bool valid = l >= 0;  // wave-uniform; every wave still reaches the barrier below
-    const LevelGeom& lg = g.lv[valid ? l : 0];
-    const uint32_t e = valid ? lvlOut[(long long)b * g.kpCap + lg.kpBase + idx] : 0u;
+    if (k >= g.kpCap || idx >= cntL) return;  // wave-uniform
     const int x = e & 0xFFF, y = (e >> 12) & 0xFFF, score = e >> 24;
     const long long fbase = lg.base + (long long)b * lg.fstride;
+    const int spw = lg.pitch >> 2;
     // raw 31x31 patch, rows y-15..y+15, cols x-15..x+15 (dword-aligned spans)
     const uint8_t* p0 = pyr + fbase + (long long)(y + EDGE - HALF_PATCH) * lg.pitch + (x + EDGE - HALF_PATCH);
     const int sh = (int)((uintptr_t)p0 & 3);
     const uint32_t* w0 = (const uint32_t*)(p0 - sh);
-    const int spw = lg.pitch >> 2;
+    // descriptor window, rows y-18..y+18, cols x-18..x+18 (inside the padded level: x, y lie in
+    // the detection region and ringX1/Y1 <= w/h + 12)
+    const uint8_t* q0 = blur + fbase + (long long)(y + EDGE - DW_R) * lg.pitch + (x + EDGE - DW_R);
+    const int wsh = (int)((uintptr_t)q0 & 3);
+    const uint32_t* v0 = (const uint32_t*)(q0 - wsh);
     uint32_t* P = s_patch[wave];
-    if (valid)
-        for (int i = lane; i < 31 * 9; i += 64) {
-            const int r = i / 9, c = i - r * 9;
-            P[r * (IC_P / 4) + c] = w0[(long long)r * spw + c];
-        }
-    __syncthreads();
-    if (!valid) return;
+    uint32_t* Q = s_win[wave];
+    constexpr int NP = (31 * 9 + 63) / 64, NW = ((2 * DW_R + 1) * 10 + 63) / 64;
+    uint32_t pv[NP], wv[NW];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+        const int i = lane + 64 * j, r = i / 9, c = i - r * 9;
+        pv[j] = i < 31 * 9 ? w0[(long long)r * spw + c] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {
+        const int i = lane + 64 * j, r = i / 10, c = i - r * 10;
+        wv[j] = i < (2 * DW_R + 1) * 10 ? v0[(long long)r * spw + c] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+        const int i = lane + 64 * j, r = i / 9, c = i - r * 9;
+        if (i < 31 * 9) P[r * (IC_P / 4) + c] = pv[j];
+    }
+#pragma unroll
+    for (int j = 0; j < NW; ++j) {
+        const int i = lane + 64 * j, r = i / 10, c = i - r * 10;
+        if (i < (2 * DW_R + 1) * 10) Q[r * (DW_P / 4) + c] = wv[j];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS is in order per wave; compiler fence
     const uint8_t* Pb = (const uint8_t*)P + sh + HALF_PATCH;  // Pb[r * IC_P + u], u in [-15, 15]
     // IC_Angle (ORBextractor.cc:124-151): lanes 0..30 take rows v = lane - 15
     int m01 = 0, m10 = 0;
@@ -1207,9 +1318,7 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
     float sa, ca;
     glibc_sincosf(angle * factorPI, &sa, &ca);
     const float a = ca, bsin = sa;
-    // the descriptor image covers every sample a keypoint of this level can reach (ringX1/Y1)
-    const uint8_t* center = blur + fbase + (long long)(y + EDGE) * lg.pitch + (x + EDGE);
-    const int pitch = lg.pitch;
+    const uint8_t* center = (const uint8_t*)Q + wsh + DW_R * DW_P + DW_R;
     int vals[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -1217,13 +1326,13 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
         const float px = (float)c_pattern[2 * pt], py = (float)c_pattern[2 * pt + 1];
         const int dy = (int)rintf(__builtin_fmaf(px, bsin, py * a));
         const int dx = (int)rintf(__builtin_fmaf(px, a, -(py * bsin)));
-        vals[q] = center[(long long)dy * pitch + dx];
+        vals[q] = center[dy * DW_P + dx];
     }
     int nib = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) nib |= (vals[2 * q] < vals[2 * q + 1]) << q;
     const int other = __shfl_xor(nib, 1, 64);
-    const long long kslot = (long long)b * g.kpCap + k;
+    const long long kslot = (long long)b * g.kpCap + before + idx;
     if ((lane & 1) == 0) desc[kslot * 32 + (lane >> 1)] = (uint8_t)(nib | (other << 4));
     if (lane == 0) {
         orb_keypoint_t kp;
@@ -1231,7 +1340,7 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
         kp.y = l == 0 ? (float)y : (float)y * lg.scale;
         kp.size = lg.size;
         kp.angle = angle;
-        kp.response = lvlResp ? lvlResp[(long long)b * g.kpCap + lg.kpBase + idx] : (float)score;
+        kp.response = lvlResp ? lvlResp[(long long)b * g.kpCap + k] : (float)score;
         kp.octave = l;
         kp.class_id = -1;
         kps[kslot] = kp;
@@ -1624,6 +1733,7 @@ struct orb_extractor {
     // per-stage HIP-event timing (orb_profile_*): stage k brackets its kernel(s) on the launch stream
     static constexpr int kStages = 5;
     bool prof = false;
+    unsigned profMask = 0;           // stages that record events (bit k = stage k)
     std::vector<hipEvent_t> evPool;  // 2 per stage per launch, recycled after each read
     std::vector<std::pair<int, int>> evPending;  // (stage, index of the start event)
     double stageMs[kStages] = {};
@@ -1861,6 +1971,16 @@ struct orb_extractor {
                 short b0 = satS16(cvRoundH((1.f - fy) * 2048)), b1 = satS16(cvRoundH(fy * 2048));
                 beta[dy] = (int)(uint16_t)b0 | ((int)(uint16_t)b1 << 16);
             }
+            for (int dx = 0; dx < dw; ++dx) {  // k_pyr_resize's no-saturation premise
+                const int c0 = alpha[dx] & 0xFFFF, c1 = (alpha[dx] >> 16) & 0xFFFF;
+                if ((short)c0 < 0 || (short)c1 < 0 || c0 + c1 > 2050)
+                    return set_err(ORB_ENOTSUP, "resize coefficient outside [0, 2050]");
+            }
+            for (int dy = 0; dy < dh; ++dy) {
+                const int c0 = beta[dy] & 0xFFFF, c1 = (beta[dy] >> 16) & 0xFFFF;
+                if ((short)c0 < 0 || (short)c1 < 0 || c0 + c1 > 2050)
+                    return set_err(ORB_ENOTSUP, "resize coefficient outside [0, 2050]");
+            }
             int xs = 0;
             while (xs <= dw - 16) xs += 16;
             while (xs < dw - 4) xs += 4;
@@ -1889,12 +2009,12 @@ struct orb_extractor {
                         r0 = std::min(r0, std::min(std::max(yofs[ly], 0), sh - 1));
                         r1 = std::max(r1, std::min(std::max(yofs[ly] + 1, 0), sh - 1));
                     }
-                    const int cs = c0 & ~3, words = ((c1 - cs) >> 2) + 1, nr = r1 - r0 + 1;
+                    const int cs = c0 & ~15, units = ((c1 - cs) >> 4) + 1, nr = r1 - r0 + 1;
                     rt.push_back(cs);
-                    rt.push_back(words);
+                    rt.push_back(units);
                     rt.push_back(r0);
                     rt.push_back(nr);
-                    lds = std::max(lds, (size_t)words * 4 * nr);
+                    lds = std::max(lds, (size_t)units * 16 * nr);
                 }
             if (lds > 96 * 1024) return set_err(ORB_ENOTSUP, "scale factor too large for the resize tile");
             resizeLds[l] = lds;
@@ -1951,15 +2071,15 @@ struct orb_extractor {
         return evPool[evNext++];
     }
     void stage_begin(int stage, hipStream_t st) {
-        if (!prof) return;
+        if (!prof || !((profMask >> stage) & 1u)) return;
         int i = evNext;
         hipEvent_t a = next_event(), b = next_event();
         if (!a || !b) return;
         hipEventRecord(a, st);
         evPending.push_back({stage, i});
     }
-    void stage_end(hipStream_t st) {
-        if (!prof || evPending.empty()) return;
+    void stage_end(int stage, hipStream_t st) {
+        if (!prof || !((profMask >> stage) & 1u) || evPending.empty()) return;
         hipEventRecord(evPool[evPending.back().second + 1], st);
     }
     int profile_collect() {
@@ -1986,24 +2106,25 @@ struct orb_extractor {
             const LevelGeom& lg = g.lv[0];
             dim3 grid((lg.pitch / 4 + 63) / 64, (lg.ph + 3) / 4, B);
             if (cn == 1)
-                hipLaunchKernelGGL(k_pyr0, grid, dim3(64, 4), 0, st, d_imgs, stride, fpitch, d_pyr, g);
+                hipLaunchKernelGGL(k_pyr0, dim3(((lg.pitch >> 4) * lg.ph + 255) / 256, B), dim3(256), 0, st, d_imgs,
+                                   stride, fpitch, d_pyr, g);
             else  // R2Y on the red channel, B2Y on the blue one
                 hipLaunchKernelGGL(k_pyr0_color, grid, dim3(64, 4), 0, st, d_imgs, stride, fpitch, cn,
                                    rgb ? 4899 : 1868, rgb ? 1868 : 4899, d_pyr, g);
         }
-        stage_end(st);
+        stage_end(0, st);
         stage_begin(1, st);
         for (int l = 1; l < nlevels; ++l) {
             const LevelGeom& lg = g.lv[l];
             dim3 grid((lg.pitch + RZ_TW - 1) / RZ_TW, (lg.ph + RZ_TH - 1) / RZ_TH, B);
             hipLaunchKernelGGL(k_pyr_resize, grid, dim3(256), resizeLds[l], st, d_pyr, d_rtab, g, l);
         }
-        stage_end(st);
+        stage_end(1, st);
         stage_begin(2, st);
         HIP_TRY(hipMemsetAsync(d_cellCount, 0, (size_t)g.nCells * B * 4, st));
         hipLaunchKernelGGL(k_level, dim3(nTiles, B), dim3(256), 0, st, d_pyr, d_blur, g, d_tiles, d_cells, d_cand,
                            d_cellCount);
-        stage_end(st);
+        stage_end(2, st);
         stage_begin(3, st);
         if (scoreType == ORB_HARRIS_SCORE)
             hipLaunchKernelGGL(k_select<true>, dim3(nlevels, B), dim3(256), selectLds, st, d_pyr, d_cand, d_cand2,
@@ -2011,12 +2132,12 @@ struct orb_extractor {
         else
             hipLaunchKernelGGL(k_select<false>, dim3(nlevels, B), dim3(256), selectLds, st, d_pyr, d_cand, d_cand2,
                                d_cellCount, g, d_cells, d_lvl, d_lvlCount, (uint64_t*)nullptr, (float*)nullptr, 0.f);
-        stage_end(st);
+        stage_end(3, st);
         stage_begin(4, st);
         dim3 gd((std::max(kpCap, 1) + 3) / 4, B);
         hipLaunchKernelGGL(k_orient_desc, gd, dim3(256), 0, st, d_pyr, d_blur, g, d_lvl, d_lvlCount, kps, desc,
                            counts, (const float*)d_lvlResp);
-        stage_end(st);
+        stage_end(4, st);
         HIP_TRY(hipGetLastError());
         return ORB_OK;
     }
@@ -2339,11 +2460,16 @@ int orb_search_for_initialization(const orb_keypoint_t* kps1, const uint8_t* des
 static const char* kStageNames[] = {"k_pyr0", "k_pyr_resize", "k_level", "k_select", "k_orient_desc"};
 
 int orb_profile_enable(orb_extractor_t* h, int enable) {
+    return orb_profile_enable_stages(h, enable ? (1u << orb_extractor::kStages) - 1u : 0u);
+}
+
+int orb_profile_enable_stages(orb_extractor_t* h, unsigned stage_mask) {
     if (!h) return set_err(ORB_EINVAL, "bad handle");
     HIP_TRY(hipSetDevice(h->device));
     int r = h->profile_collect();
     if (r) return r;
-    h->prof = enable != 0;
+    h->profMask = stage_mask & ((1u << orb_extractor::kStages) - 1u);
+    h->prof = h->profMask != 0;
     for (int k = 0; k < orb_extractor::kStages; ++k) {
         h->stageMs[k] = 0;
         h->stageLaunches[k] = 0;

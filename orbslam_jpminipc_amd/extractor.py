@@ -167,6 +167,14 @@ class ORBextractor:
         """Record a HIP-event pair around every kernel stage of extract_batch_device."""
         check(self._lib.orb_profile_enable(self._h, int(enable)))
 
+    def profile_enable_stages(self, stages) -> None:
+        """Record event pairs around the named stages only (each pair is a stream boundary)."""
+        names = [self._lib.orb_profile_stage_name(i).decode() for i in range(16)]
+        mask = 0
+        for s in stages:
+            mask |= 1 << names.index(s)
+        check(self._lib.orb_profile_enable_stages(self._h, mask))
+
     def profile_read(self) -> dict:
         """{stage_name: (cumulative_ms, launches)} since profile_enable (synchronises)."""
         ms = np.zeros(16, np.float64)
