@@ -639,6 +639,40 @@ __device__ __forceinline__ float harris_response(const uint8_t* roi, int pitch, 
     return rsp * scale4;
 }
 
+// Exclusive prefix of src[0..n) into dst[0..n], total into dst[n], on one wave (n <= 256).
+__device__ __forceinline__ void wave_prefix(int* dst, const int* src, int n, int lane) {
+    int carry = 0;
+    for (int c0 = 0; c0 < n; c0 += 64) {
+        const int c = c0 + lane;
+        const int v = c < n ? src[c] : 0;
+        int incl = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int nb = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += nb;
+        }
+        if (c < n) dst[c] = carry + incl - v;
+        carry += __shfl(incl, 63, 64);
+    }
+    if (lane == 0) dst[n] = carry;
+}
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Cell of list element i: the last c in [0, n) with off[c] <= i (off ascending, off[0] = 0).
+__device__ __forceinline__ int cell_of(const int* off, int n, int i) {
+    int lo = 0, hi = n;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (off[mid] <= i) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
 template <bool HARRIS>
 __global__ void __launch_bounds__(256) k_select(const uint8_t* __restrict__ pyr, uint32_t* __restrict__ cand,
                                                 uint32_t* __restrict__ cand2, int* __restrict__ cellCount, Geom g,
@@ -652,23 +686,40 @@ __global__ void __launch_bounds__(256) k_select(const uint8_t* __restrict__ pyr,
     __shared__ int s_koff[ORB_MAX_CELLS_PER_LEVEL + 1];
     __shared__ uint8_t s_skip[ORB_MAX_CELLS_PER_LEVEL];
     __shared__ int s_fb[ORB_MAX_CELLS_PER_LEVEL + 1];  // cells to re-run at t = 7, count last
-    const int l = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    __shared__ int s_coff[ORB_MAX_CELLS_PER_LEVEL];    // candOff of every cell
+    const int l = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const LevelGeom& lg = g.lv[l];
     const int nC = lg.rows * lg.cols;
     const CellGeom* lc = cells + lg.cell0;
     uint32_t* fcand = cand + (long long)b * g.candPerFrame;
     int* fcount = cellCount + (long long)b * g.nCells + lg.cell0;
-    if (tid < 64) {  // counts, skip flags, and the list of cells to re-run (ascending)
+    if (wave == 0) {  // counts, skip flags, and the list of cells to re-run (ascending)
+        constexpr int CPL = ORB_MAX_CELLS_PER_LEVEL / 64;
+        int cnt[CPL], cap[CPL], skip[CPL], hx[CPL], hy[CPL], coff[CPL];
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) {  // every load of the wave in flight at once
+            const int c = 64 * j + lane;
+            if (c < nC) {
+                cnt[j] = fcount[c];
+                cap[j] = lc[c].cap;
+                skip[j] = lc[c].skipped;
+                hx[j] = lc[c].hx;
+                hy[j] = lc[c].hy;
+                coff[j] = lc[c].candOff;
+            }
+        }
         int nfb = 0;
-        for (int c0 = 0; c0 < nC; c0 += 64) {
-            const int c = c0 + lane;
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) {
+            const int c = 64 * j + lane;
             bool fb = false;
             if (c < nC) {
-                const CellGeom& cg = lc[c];
-                const int n = (cg.skipped || cg.hx <= 6 || cg.hy <= 6) ? 0 : min(fcount[c], cg.cap);
+                const int n = (skip[j] || hx[j] <= 6 || hy[j] <= 6) ? 0 : min(cnt[j], cap[j]);
                 s_cnt[c] = n;
-                s_skip[c] = (uint8_t)cg.skipped;
-                fb = !cg.skipped && n <= 3;
+                s_skip[c] = (uint8_t)skip[j];
+                s_coff[c] = coff[j];
+                fb = !skip[j] && n <= 3;
             }
             const uint64_t m = __ballot(fb);
             if (fb) s_fb[nfb + __popcll(m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))))] = c;
@@ -697,48 +748,62 @@ __global__ void __launch_bounds__(256) k_select(const uint8_t* __restrict__ pyr,
             __syncthreads();
         }
     }
-    if (tid == 0) {
-        int s = 0;
-        for (int c = 0; c < nC; ++c) {
-            s_off[c] = s;
-            s += s_cnt[c];
-        }
-        s_off[nC] = s;
-        // (3) nToRetain / nToDistribute / bNoMore bookkeeping (ORBextractor.cc:622-670)
+    if (wave == 0) {
+        wave_prefix(s_off, s_cnt, nC, lane);
+        // (3) nToRetain / nToDistribute / bNoMore bookkeeping (ORBextractor.cc:622-670), one
+        // lane per cell: within a pass every cell's update reads only the pass constants, and
+        // the pass totals are integer sums, so the lanes reproduce the sequential loop exactly.
+        // A skipped cell keeps 0 and is not bNoMore after the first pass (the reference
+        // `continue`s past it), then takes the tot = 0 branch of the redistribution.
+        constexpr int CPL = ORB_MAX_CELLS_PER_LEVEL / 64;
         const int nfc = lg.nfc;
-        int nNoMore = 0, nToDistribute = 0;
-        unsigned long long noMore[(ORB_MAX_CELLS_PER_LEVEL + 63) / 64] = {};
-        for (int c = 0; c < nC; ++c) {
-            if (s_skip[c]) {
-                s_ret[c] = 0;
-                continue;
-            }
-            const int nKeys = s_cnt[c];
-            if (nKeys > nfc) {
-                s_ret[c] = nfc;
-            } else {
-                s_ret[c] = nKeys;
-                nToDistribute += nfc - nKeys;
-                noMore[c >> 6] |= 1ull << (c & 63);
-                nNoMore++;
-            }
-        }
-        while (nToDistribute > 0 && nNoMore < nC) {
-            const int nNew = nfc + (int)ceilf((float)nToDistribute / (nC - nNoMore));
-            nToDistribute = 0;
-            for (int c = 0; c < nC; ++c) {
-                if (noMore[c >> 6] & (1ull << (c & 63))) continue;
-                const int tot = s_skip[c] ? 0 : s_cnt[c];
-                if (tot > nNew) {
-                    s_ret[c] = nNew;
+        int ret[CPL], tot[CPL];
+        bool more[CPL];  // live and not bNoMore
+        int dist = 0, nm = 0;
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) {
+            const int c = 64 * j + lane;
+            more[j] = false;
+            ret[j] = 0;
+            tot[j] = 0;
+            if (c < nC) {
+                const bool sk = s_skip[c] != 0;
+                tot[j] = sk ? 0 : s_cnt[c];
+                if (sk) {
+                    more[j] = true;
+                } else if (tot[j] > nfc) {
+                    ret[j] = nfc;
+                    more[j] = true;
                 } else {
-                    s_ret[c] = tot;
-                    nToDistribute += nNew - tot;
-                    noMore[c >> 6] |= 1ull << (c & 63);
-                    nNoMore++;
+                    ret[j] = tot[j];
+                    dist += nfc - tot[j];
+                    nm++;
                 }
             }
         }
+        int nToDistribute = wave_sum(dist), nNoMore = wave_sum(nm);
+        while (nToDistribute > 0 && nNoMore < nC) {
+            const int nNew = nfc + (int)ceilf((float)nToDistribute / (nC - nNoMore));
+            dist = 0;
+            nm = 0;
+#pragma unroll
+            for (int j = 0; j < CPL; ++j) {
+                if (!more[j]) continue;
+                if (tot[j] > nNew) {
+                    ret[j] = nNew;
+                } else {
+                    ret[j] = tot[j];
+                    dist += nNew - tot[j];
+                    more[j] = false;
+                    nm++;
+                }
+            }
+            nToDistribute = wave_sum(dist);
+            nNoMore += wave_sum(nm);
+        }
+#pragma unroll
+        for (int j = 0; j < CPL; ++j)
+            if (64 * j + lane < nC) s_ret[64 * j + lane] = ret[j];
     }
     __syncthreads();
     const int M = s_off[nC];
@@ -746,21 +811,46 @@ __global__ void __launch_bounds__(256) k_select(const uint8_t* __restrict__ pyr,
     uint32_t* raw = (uint32_t*)smem;                                      // arrival order
     uint32_t* srt = inLds ? raw + SELECT_CAP : cand2 + (long long)b * g.candPerFrame;  // raster order
     const uint32_t* srcOf = inLds ? raw : fcand;
-    if (inLds) {
-        for (int c = wave; c < nC; c += 4)
-            for (int k = lane; k < s_cnt[c]; k += 64) raw[s_off[c] + k] = fcand[lc[c].candOff + k];
+    if (inLds) {  // the level's survivors, cell after cell, one element per thread (4 loads in flight)
+        for (int i0 = tid; i0 < M; i0 += 1024) {
+            uint32_t v[4];
+            int dsti[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = i0 + 256 * u;
+                dsti[u] = -1;
+                if (i < M) {
+                    const int c = cell_of(s_off, nC, i);
+                    v[u] = fcand[s_coff[c] + (i - s_off[c])];
+                    dsti[u] = i;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (dsti[u] >= 0) raw[dsti[u]] = v[u];
+        }
         __syncthreads();
-    }
-    // (2) rank sort of each cell by position (positions are unique)
-    for (int c = wave; c < nC; c += 4) {
-        const int n = s_cnt[c];
-        const uint32_t* seg = srcOf + (inLds ? s_off[c] : lc[c].candOff);
-        uint32_t* dst = srt + (inLds ? s_off[c] : lc[c].candOff);
-        for (int i = lane; i < n; i += 64) {
-            const uint32_t e = seg[i], key = e & 0xFFFFFFu;
+        // (2) rank sort of each cell by position (positions are unique), one element per thread
+        for (int i = tid; i < M; i += 256) {
+            const int c = cell_of(s_off, nC, i);
+            const int o = s_off[c], n = s_cnt[c];
+            const uint32_t e = raw[i], key = e & 0xFFFFFFu;
             int r = 0;
-            for (int j2 = 0; j2 < n; ++j2) r += (seg[j2] & 0xFFFFFFu) < key;
-            dst[r] = e;
+            for (int j2 = 0; j2 < n; ++j2) r += (raw[o + j2] & 0xFFFFFFu) < key;
+            srt[o + r] = e;
+        }
+    } else {
+        // (2) as above on the frame's scratch area, one wave per cell
+        for (int c = wave; c < nC; c += 4) {
+            const int n = s_cnt[c];
+            const uint32_t* seg = srcOf + lc[c].candOff;
+            uint32_t* dst = srt + lc[c].candOff;
+            for (int i = lane; i < n; i += 64) {
+                const uint32_t e = seg[i], key = e & 0xFFFFFFu;
+                int r = 0;
+                for (int j2 = 0; j2 < n; ++j2) r += (seg[j2] & 0xFFFFFFu) < key;
+                dst[r] = e;
+            }
         }
     }
     __syncthreads();
@@ -784,14 +874,7 @@ __global__ void __launch_bounds__(256) k_select(const uint8_t* __restrict__ pyr,
             s_cnt[c] = orbsel::retain_best(seg, s_cnt[c], s_ret[c], hcomp);
         }
         __syncthreads();
-        if (tid == 0) {
-            int s = 0;
-            for (int c = 0; c < nC; ++c) {
-                s_koff[c] = s;
-                s += s_cnt[c];
-            }
-            s_koff[nC] = s;
-        }
+        if (wave == 0) wave_prefix(s_koff, s_cnt, nC, lane);
         __syncthreads();
         const int K = s_koff[nC];
         uint64_t* list;
@@ -830,20 +913,15 @@ __global__ void __launch_bounds__(256) k_select(const uint8_t* __restrict__ pyr,
         s_cnt[c] = KS_SKIP_RETAIN ? min(s_cnt[c], max(s_ret[c], 0)) : orbsel::retain_best(seg, s_cnt[c], s_ret[c], comp);
     }
     __syncthreads();
-    if (tid == 0) {
-        int s = 0;
-        for (int c = 0; c < nC; ++c) {
-            s_koff[c] = s;
-            s += s_cnt[c];
-        }
-        s_koff[nC] = s;
-    }
+    if (wave == 0) wave_prefix(s_koff, s_cnt, nC, lane);
     __syncthreads();
     const int K = s_koff[nC];
     uint32_t* list;
-    if (inLds) {  // kept prefixes of srt -> raw (disjoint regions)
-        for (int c = wave; c < nC; c += 4)
-            for (int k = lane; k < s_cnt[c]; k += 64) raw[s_koff[c] + k] = srt[s_off[c] + k];
+    if (inLds) {  // kept prefixes of srt -> raw (disjoint regions), one element per thread
+        for (int i = tid; i < K; i += 256) {
+            const int c = cell_of(s_koff, nC, i);
+            raw[i] = srt[s_off[c] + (i - s_koff[c])];
+        }
         list = raw;
     } else {  // sequential in-place compaction (dest <= src, ascending) in cand2's level area
         list = srt + lc[0].candOff;
