@@ -687,7 +687,9 @@ __global__ void __launch_bounds__(256) k_select(const uint8_t* __restrict__ pyr,
     __shared__ uint8_t s_skip[ORB_MAX_CELLS_PER_LEVEL];
     __shared__ int s_fb[ORB_MAX_CELLS_PER_LEVEL + 1];  // cells to re-run at t = 7, count last
     __shared__ int s_coff[ORB_MAX_CELLS_PER_LEVEL];    // candOff of every cell
-    const int l = blockIdx.x, b = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+    // grid (frame, level): workgroup i runs on XCD i % 8, so every XCD gets every level (with
+    // (level, frame) all the heavy level-0 lists landed on one XCD), heaviest level first
+    const int b = blockIdx.x, l = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const LevelGeom& lg = g.lv[l];
     const int nC = lg.rows * lg.cols;
@@ -2205,10 +2207,10 @@ struct orb_extractor {
         stage_end(2, st);
         stage_begin(3, st);
         if (scoreType == ORB_HARRIS_SCORE)
-            hipLaunchKernelGGL(k_select<true>, dim3(nlevels, B), dim3(256), selectLds, st, d_pyr, d_cand, d_cand2,
+            hipLaunchKernelGGL(k_select<true>, dim3(B, nlevels), dim3(256), selectLds, st, d_pyr, d_cand, d_cand2,
                                d_cellCount, g, d_cells, d_lvl, d_lvlCount, d_candH, d_lvlResp, harrisScale4);
         else
-            hipLaunchKernelGGL(k_select<false>, dim3(nlevels, B), dim3(256), selectLds, st, d_pyr, d_cand, d_cand2,
+            hipLaunchKernelGGL(k_select<false>, dim3(B, nlevels), dim3(256), selectLds, st, d_pyr, d_cand, d_cand2,
                                d_cellCount, g, d_cells, d_lvl, d_lvlCount, (uint64_t*)nullptr, (float*)nullptr, 0.f);
         stage_end(3, st);
         stage_begin(4, st);
