@@ -4,7 +4,11 @@
 A step = one pass of the hot path over one batch of B synthetic 640x480 frames resident in
 HBM: ORBextractor(1000, 1.2, 8, FAST, 20) on all B frames (orb_extract_batch_device), then
 ORBmatcher(0.9, true).SearchForInitialization(F_t, F_t+1, window 100) on the B-1
-consecutive pairs (orb_search_for_initialization_batch_device).  N GPUs run N independent
+consecutive pairs (orb_search_for_initialization_batch_device), on one stream.  --overlap 1
+runs the steps as a two-stage stream pipeline instead (step t extracts batch t while batch t-1
+is matched on a second stream; the serial step is then reported beside it as "serial_step"):
+measured equal to the serial step on MI355X (1.80 vs 1.79 ms), so it is off by default.
+N GPUs run N independent
 replicas (frames shard one stream per GPU; no collectives on the data path); value is the
 whole-job frames/s = N * B * K / max-over-ranks(time of K steps).
 
@@ -114,6 +118,8 @@ def main():
     ap.add_argument("--nfeatures", type=int, default=1000)
     ap.add_argument("--cpu-frames", type=int, default=3072,
                     help="CPU-baseline sample size (0 = skip); ~20 s of CPU-thread time on 16 threads")
+    ap.add_argument("--overlap", type=int, default=0,
+                    help="1: extract(t) on one stream while matching batch t-1 on another; 0: serial step")
     ap.add_argument("--survey-steps", type=int, default=5, help="untimed steps with every stage bracketed")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = OMP_NUM_THREADS or os.cpu_count()")
     args = ap.parse_args()
@@ -137,29 +143,72 @@ def main():
     d_cnt = torch.empty((B,), dtype=torch.int32, device="cuda")
     f1 = torch.arange(0, B - 1, dtype=torch.int32, device="cuda")
     f2 = f1 + 1
-    # one stream carries the whole step: extraction, then the matching that reads its output
-    stream = torch.cuda.Stream()
+    # serial mode: one stream carries the whole step, extraction then the matching that reads
+    # its output.  overlap mode (default): a two-stage stream pipeline over consecutive batches —
+    # step t extracts batch t on s_ext while s_match runs SearchForInitialization on batch t-1
+    # (double-buffered outputs, event-ordered); every step still does B extractions and B-1
+    # pair matches, so steps/s is the same work rate.
+    s_ext = torch.cuda.Stream()
+    s_match = torch.cuda.Stream()
     torch.cuda.current_stream().synchronize()  # inputs uploaded on the default stream
+    bufs = [(d_kps, d_desc, d_cnt),
+            (torch.empty_like(d_kps), torch.empty_like(d_desc), torch.empty_like(d_cnt))]
+    ev_edone = [torch.cuda.Event(), torch.cuda.Event()]
+    ev_mdone = [torch.cuda.Event(), torch.cuda.Event()]
     ev_m = []
+    st = {"t": 0, "overlap": False}
+
+    def match(kps, desc, cnt, stream, timed):
+        if timed:
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+        m12, nm = matcher.search_for_initialization_batch_device(kps, desc, cnt, f1, f2, W, H, 100, stream=stream)
+        if timed:
+            b.record(stream)
+            ev_m.append((a, b))
+        return nm
 
     def step(timed=False):
-        with torch.cuda.stream(stream):
-            ext.extract_batch_device(d_imgs, d_kps, d_desc, d_cnt, stream=stream)
-            if timed:
-                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                a.record(stream)
-            m12, nm = matcher.search_for_initialization_batch_device(d_kps, d_desc, d_cnt, f1, f2, W, H, 100,
-                                                                     stream=stream)
-            if timed:
-                b.record(stream)
-                ev_m.append((a, b))
+        if not st["overlap"]:
+            with torch.cuda.stream(s_ext):
+                ext.extract_batch_device(d_imgs, d_kps, d_desc, d_cnt, stream=s_ext)
+                return match(d_kps, d_desc, d_cnt, s_ext, timed)
+        t = st["t"]
+        st["t"] += 1
+        cur, prev = t % 2, (t - 1) % 2
+        with torch.cuda.stream(s_ext):
+            if t >= 2:
+                s_ext.wait_event(ev_mdone[cur])  # match(t-2) has read this buffer
+            ext.extract_batch_device(d_imgs, *bufs[cur], stream=s_ext)
+            ev_edone[cur].record(s_ext)
+        nm = None
+        if t >= 1:
+            with torch.cuda.stream(s_match):
+                s_match.wait_event(ev_edone[prev])
+                nm = match(*bufs[prev], s_match, timed)
+                ev_mdone[prev].record(s_match)
         return nm
+
+    def timed_run(overlap, time_match):
+        st["overlap"], st["t"] = overlap, 0
+        if overlap:
+            step()  # fill the pipeline: batch 0 extracted, its match runs in the first timed step
+        torch.cuda.synchronize()
+        replicas.barrier(info)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            nm = step(timed=time_match)
+        torch.cuda.synchronize()
+        replicas.barrier(info)
+        return time.perf_counter() - t0, nm
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    # stage survey (untimed): an event pair around every stage gives the per-stage table; each
-    # pair is a stream boundary (~10 us), so the timed run below brackets only the dominant stage
+    # stage survey (untimed, serial): an event pair around every stage gives the per-stage
+    # table; each pair is a stream boundary (~10 us), so the timed run below brackets only the
+    # dominant stage
     ext.profile_enable(True)
     for _ in range(args.survey_steps):
         step(timed=True)
@@ -170,17 +219,12 @@ def main():
     ev_m.clear()
     dom = max(survey, key=lambda k: survey[k][0])
     time_match = dom == "k_match_init"
+    if args.overlap:  # the serial step, for reference (no events)
+        serial_elapsed, _ = timed_run(False, False)
+        serial_tmax = replicas.max_over_ranks(serial_elapsed, info)
     if not time_match:
         ext.profile_enable_stages([dom])
-    replicas.barrier(info)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        nm = step(timed=time_match)
-    torch.cuda.synchronize()
-    replicas.barrier(info)
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
+    elapsed, nm = timed_run(args.overlap, time_match)
     if time_match:
         live = (sum(a.elapsed_time(b) for a, b in ev_m), len(ev_m))
     else:
@@ -260,8 +304,11 @@ def main():
                         f"nnratio 0.9 checkOri window 100 (BASELINE.json configs[1]+[2])",
             "batch_per_gpu": B,
             "pairs_per_gpu": B - 1,
-            "parallelism": f"replicas x{world} (one stream per GPU, no collectives)",
+            "parallelism": f"replicas x{world} (no collectives)",
+            "streams": "extract(t) || SearchForInitialization(t-1), double-buffered" if args.overlap
+                       else "one stream, extract then match",
         },
+
         "roofline": {
             "kernel": dom,
             "bound": "hbm",
@@ -283,6 +330,9 @@ def main():
         "workload_stats": {"keypoints_per_frame": n_kp / B, "fast_survivors_per_frame": n_cand / B,
                            "matches_per_pair": float(nm_h.mean())},
     }
+    if args.overlap:
+        result["serial_step"] = {"value": replicas.whole_job_rate(B * args.steps, world, serial_tmax),
+                                 "ms_per_step": serial_tmax / args.steps * 1e3}
     if rank == 0 and world == 1 and args.cpu_frames > 0:
         threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or os.cpu_count())
         ncpu = args.cpu_frames
