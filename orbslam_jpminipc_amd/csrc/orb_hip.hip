@@ -284,8 +284,10 @@ __device__ __forceinline__ void stage_rows_to_lds(uint32_t* __restrict__ dst, in
 // no intermediate of the reference's saturating chain can saturate: H <= 255 * 2050 = 522750,
 // (H >> 4) * b < 2^27, the SSE2 sum <= 1023 and the scalar sum < 2^31; both end in [0, 255].
 // The SSE2 path's (h * b) >> 16 is then mulhi(h, b << 16).
-#define RZ_TW 256
-#define RZ_TH 64
+#define RZ_TW 256  // 64 lanes x 4 columns
+#ifndef RZ_TH
+#define RZ_TH 32
+#endif
 __global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, const int* __restrict__ rtab, Geom g,
                                                     int l) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_src[];
