@@ -126,6 +126,12 @@ struct CellGeom {
 using namespace orbdev;
 
 __constant__ signed char c_pattern[1024];
+#ifndef KL_COUNT
+#define KL_COUNT 0
+#endif
+#if KL_COUNT
+__device__ unsigned long long g_klcount[4];  // lane-rows queued, pixels expanded, corners, survivors
+#endif
 
 // ---- pyramid --------------------------------------------------------------------------
 // Level 0: copyMakeBorder(image, 16, BORDER_REFLECT_101); one thread per 16-byte chunk of a
@@ -1197,6 +1203,12 @@ __global__ void __launch_bounds__(256) k_level(const uint8_t* __restrict__ pyr, 
                 np += __popcll(m);
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#if KL_COUNT
+            if (lane == 0) {
+                atomicAdd(&g_klcount[0], (unsigned long long)min(64, qn - i0));
+                atomicAdd(&g_klcount[1], (unsigned long long)np);
+            }
+#endif
             int cn = 0;
             for (int p0 = 0; p0 < np; p0 += 64) {
                 bool corner = false;
@@ -1210,6 +1222,9 @@ __global__ void __launch_bounds__(256) k_level(const uint8_t* __restrict__ pyr, 
                 cn += __popcll(m);
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#if KL_COUNT
+            if (lane == 0) atomicAdd(&g_klcount[2], (unsigned long long)cn);
+#endif
             for (int k = lane; k < cn; k += 64) {
                 const uint16_t c = cq[k];
                 const uint8_t* p = inb + ((c >> 9) + 3) * TP + (c & 511) + 3;
@@ -2643,6 +2658,20 @@ int orb_debug_blur_image(orb_extractor_t* h, int b, int l, uint8_t* out) {
 }
 
 // Per-cell FAST counts (after fallback) of frame `b`, level `l`, row-major cells.
+// k_level queue statistics of a -DKL_COUNT=1 build (timing experiments; 0 otherwise): reads
+// and clears {lane-rows queued, pixels expanded, corners} summed over launches.
+int orb_debug_klevel_counts(unsigned long long* out3) {
+#if KL_COUNT
+    unsigned long long z[4] = {0, 0, 0, 0};
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out3, HIP_SYMBOL(g_klcount), 3 * sizeof(unsigned long long)));
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_klcount), z, sizeof(z)));
+#else
+    out3[0] = out3[1] = out3[2] = 0;
+#endif
+    return ORB_OK;
+}
+
 int orb_debug_cell_counts(orb_extractor_t* h, int b, int l, int* counts, int cap) {
     if (!h || l < 0 || l >= h->nlevels || !h->d_cellCount) return set_err(ORB_EINVAL, "bad arguments");
     const LevelGeom& lg = h->g.lv[l];

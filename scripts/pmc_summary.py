@@ -4,18 +4,21 @@
 Usage: pmc_summary.py gpurun_out/TAG [--json OUT] [--width W --height H --batch B --nfeatures N]
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch (TCC_EA0 request counters, MI355X_MICROARCH.md
-§HBM).  The guide's ×2 FETCH correction is calibrated for 16-B/lane streaming loads only; the
-extraction kernels load dwords, so the read calibration is measured in the same run: k_pyr0
-reads exactly the B input frames (B·W·H bytes, evicted from the 256 MiB Infinity Cache by the
-~0.6 GB every step writes) with the same dword-per-lane pattern, and read_bytes = FETCH ×
-(B·W·H / FETCH(k_pyr0)) for every kernel.  WRITE_SIZE is taken as is (exact for streaming
-stores per the guide).
+§HBM).  The guide's ×2 FETCH correction holds for 16-B/lane streaming loads; it is measured in
+the same run on k_pyr0, which reads exactly the B input frames (B·W·H bytes, evicted from the
+256 MiB Infinity Cache by the ~0.6 GB every step writes) with 16-B loads, and applied to the
+16-B-load kernels (k_pyr0, k_pyr_resize).  The dword-load kernels use the factor measured the
+same way when k_pyr0 still loaded dwords (r01_v16: 1.353).  WRITE_SIZE is taken as is (exact
+for streaming stores per the guide).
 """
 import argparse
 import csv
 import glob
 import json
 from collections import defaultdict
+
+
+WIDE_LOADS = {"k_pyr0", "k_pyr_resize"}
 
 
 def main():
@@ -26,6 +29,9 @@ def main():
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--nfeatures", type=int, default=1000)
+    ap.add_argument("--dword-factor", type=float, default=1.3532485621757968,
+                    help="FETCH_SIZE calibration of dword-per-lane loads: measured on k_pyr0 when it "
+                         "loaded dwords (profiles/r01_v16_pmc.json)")
     a = ap.parse_args()
     acc = defaultdict(lambda: defaultdict(list))
     for f in sorted(glob.glob(f"{a.root}/p*/run_counter_collection.csv")):
@@ -38,12 +44,16 @@ def main():
     cal = known / (mean["k_pyr0"]["FETCH_SIZE"] * 1024.0) if "k_pyr0" in mean else None
     out = {"source": a.root.rstrip("/").split("/")[-1],
            "workload": {"width": a.width, "height": a.height, "batch": a.batch, "nfeatures": a.nfeatures},
-           "read_calibration": {"kernel": "k_pyr0", "known_read_bytes": known, "factor": cal},
+           "read_calibration": {"kernel": "k_pyr0", "known_read_bytes": known, "factor": cal,
+                                "applies_to": sorted(WIDE_LOADS), "dword_factor": a.dword_factor,
+                                "dword_factor_source": "r01_v16_pmc (k_pyr0 with dword loads)"},
            "per_launch": {}}
     for k, d in sorted(mean.items()):
         if "FETCH_SIZE" not in d or "WRITE_SIZE" not in d:
             continue
-        rd = d["FETCH_SIZE"] * 1024.0 * (cal or 1.0)
+        # k_pyr0 / k_pyr_resize load 16 B per lane (calibrated here on k_pyr0's known read, the
+        # guide's x2); the other kernels load dwords (the r01_v16 dword calibration)
+        rd = d["FETCH_SIZE"] * 1024.0 * ((cal or 1.0) if k in WIDE_LOADS else a.dword_factor)
         wr = d["WRITE_SIZE"] * 1024.0
         out["per_launch"][k] = {"fetch_kib": d["FETCH_SIZE"], "write_kib": d["WRITE_SIZE"], "read_bytes": rd,
                                 "write_bytes": wr, "hbm_bytes": rd + wr,
