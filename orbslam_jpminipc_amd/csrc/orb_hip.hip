@@ -1054,7 +1054,14 @@ __global__ void __launch_bounds__(256) k_level(const uint8_t* __restrict__ pyr, 
     __shared__ uint16_t s_px[4][LVL_CQ];  // queue entries expanded to pixels (<= 4 x 64)
     const BlurTile t = tiles[blockIdx.x];
     const int b = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const LevelGeom& lg = g.lv[t.level];
+    // the level's geometry in SGPRs for the whole kernel: read through a reference into the
+    // kernarg block, the compiler re-issued a dependent s_load per use inside the row loop
+    // (12 per row); the empty asm makes the copies opaque, so they cannot be rematerialised
+    LevelGeom lg = g.lv[t.level];
+    asm volatile("" : "+s"(lg.w), "+s"(lg.h), "+s"(lg.pitch), "+s"(lg.ph), "+s"(lg.detX1), "+s"(lg.detY1),
+                 "+s"(lg.ringX1), "+s"(lg.ringY1));
+    asm volatile("" : "+s"(lg.xsimd_blur), "+s"(lg.rows), "+s"(lg.cols), "+s"(lg.cellW), "+s"(lg.cellH),
+                 "+s"(lg.cell0), "+s"(lg.base), "+s"(lg.fstride));
     const uint8_t* src = pyr + lg.base + (long long)b * lg.fstride;
     uint8_t* dst = blur + lg.base + (long long)b * lg.fstride;
     // input rows y0-4 .. y0+TH+3 (blur: +-3; FAST ring of a halo pixel: +-4), columns
