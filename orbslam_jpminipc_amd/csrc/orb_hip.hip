@@ -219,11 +219,14 @@ __device__ __forceinline__ void stage_tile16(uint4* __restrict__ dst, const uint
     for (int base = 0; base < total; base += RZ_SB * 256) {
         const int i0 = base + tid;
         const int r0 = i0 / units, c0 = i0 - r0 * units;
+        // every slot is loaded (past-the-end slots re-read unit 0): a conditionally assigned
+        // uint4 array was placed in scratch, one private-memory round trip per tile
         uint4 v[RZ_SB];
         int r = r0, c = c0;
 #pragma unroll
         for (int k = 0; k < RZ_SB; ++k) {
-            if (i0 + k * 256 < total) v[k] = src[(long long)r * gsu + c];
+            const bool ok = i0 + k * 256 < total;
+            v[k] = src[ok ? (long long)r * gsu + c : 0ll];
             r += dr;
             c += dc;
             if (c >= units) {
@@ -294,11 +297,11 @@ __device__ __forceinline__ void stage_rows_to_lds(uint32_t* __restrict__ dst, in
 #ifndef RZ_TH
 #define RZ_TH 32
 #endif
-__global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, const int* __restrict__ rtab, Geom g,
-                                                    int l) {
+// The two levels arrive by value: a Geom indexed by the runtime level was copied to scratch
+// (144 B per lane of private-memory traffic per thread).
+__global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, const int* __restrict__ rtab,
+                                                    const LevelGeom lg, const LevelGeom ls) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_src[];
-    const LevelGeom& lg = g.lv[l];
-    const LevelGeom& ls = g.lv[l - 1];
     const int b = blockIdx.z, tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int* tt = rtab + lg.rtile + 4 * (blockIdx.y * gridDim.x + blockIdx.x);
@@ -2221,7 +2224,7 @@ struct orb_extractor {
         for (int l = 1; l < nlevels; ++l) {
             const LevelGeom& lg = g.lv[l];
             dim3 grid((lg.pitch + RZ_TW - 1) / RZ_TW, (lg.ph + RZ_TH - 1) / RZ_TH, B);
-            hipLaunchKernelGGL(k_pyr_resize, grid, dim3(256), resizeLds[l], st, d_pyr, d_rtab, g, l);
+            hipLaunchKernelGGL(k_pyr_resize, grid, dim3(256), resizeLds[l], st, d_pyr, d_rtab, g.lv[l], g.lv[l - 1]);
         }
         stage_end(1, st);
         stage_begin(2, st);
