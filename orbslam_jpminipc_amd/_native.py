@@ -14,7 +14,8 @@ import pathlib
 import numpy as np
 
 PKG_DIR = pathlib.Path(__file__).resolve().parent
-HIP_LIB_PATH = PKG_DIR / "liborb_hip.so"
+# ORB_HIP_LIB names an experiment build of the same library (scripts/build_variant.sh)
+HIP_LIB_PATH = pathlib.Path(os.environ["ORB_HIP_LIB"]) if os.environ.get("ORB_HIP_LIB") else PKG_DIR / "liborb_hip.so"
 SYNTH_LIB_PATH = PKG_DIR / "libsynth.so"
 
 # cv::KeyPoint layout (28 bytes), reference include/SaveLoadWorld.h:1406-1425
