@@ -1398,21 +1398,33 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
         if (i < (2 * DW_R + 1) * 10) Q[r * (DW_P / 4) + c] = wv[j];
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS is in order per wave; compiler fence
-    const uint8_t* Pb = (const uint8_t*)P + sh + HALF_PATCH;  // Pb[r * IC_P + u], u in [-15, 15]
-    // IC_Angle (ORBextractor.cc:124-151): lanes 0..30 take rows v = lane - 15
+    // IC_Angle (ORBextractor.cc:124-151): the disc sums m10 = sum u*I, m01 = sum v*I over
+    // |u| <= umax[|v|], one patch dword per lane and step (unit n = row * 9 + dword: the LDS
+    // index itself).  Byte i of dword c sits at u = base + i, base = 4c - sh - 15, so a dword
+    // adds base * S + sum(i * I_i) to m10 and v * S to m01, S = its in-disc byte sum: two
+    // v_dot4 on the masked dword (integer sums: the same totals in any order).
     int m01 = 0, m10 = 0;
-    if (lane < 31) {
-        const int v = lane - HALF_PATCH;
-        const int d = g.umax[v < 0 ? -v : v];
-        const uint8_t* row = Pb + lane * IC_P;
-        int su = 0, sm = 0;
-        for (int u = -d; u <= d; ++u) {
-            const int val = row[u];
-            su += u * val;
-            sm += val;
+    {
+        uint64_t umaxNib = 0;  // umax[0..15] as nibbles (wave-uniform)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) umaxNib |= (uint64_t)g.umax[i] << (4 * i);
+#pragma unroll
+        for (int j = 0; j < (31 * 9 + 63) / 64; ++j) {
+            const int n = lane + 64 * j;
+            if (n < 31 * 9) {
+                const int r = n / 9, c = n - r * 9;
+                const int v = r - HALF_PATCH;
+                const int d = (int)(umaxNib >> (4 * (v < 0 ? -v : v))) & 15;
+                const int base = 4 * c - sh - HALF_PATCH;
+                const int ilo = max(0, -d - base), ihi = min(3, d - base);
+                const uint32_t mask = ilo > ihi ? 0u : ((0xFFFFFFFFu >> (8 * (3 - ihi))) & (0xFFFFFFFFu << (8 * ilo)));
+                const uint32_t pm = P[n] & mask;
+                const int S = (int)__builtin_amdgcn_udot4(pm, 0x01010101u, 0u, false);
+                const int T = (int)__builtin_amdgcn_udot4(pm, 0x03020100u, 0u, false);
+                m10 += base * S + T;
+                m01 += v * S;
+            }
         }
-        m10 = su;
-        m01 = v * sm;
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
