@@ -421,37 +421,40 @@ __global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, c
 //           detection region, and non-corners, score 0 — cv::FAST on a cell-sized Mat
 // then the survivors are compacted in raster order as (score << 24) | (y << 12) | x.
 
+typedef short i16x2_t __attribute__((ext_vector_type(2)));
 // cv::FAST corner test at threshold t: >= 9 contiguous circle pixels all > v+t or all < v-t.
+// Packed 16-bit arithmetic: circle points k and k + 8 share a dword; the sign bits of
+// (v + t) - c and c - (v - t) are the bright / dark flags (values within i16 for any t <= 255).
+// About 70 VALU instead of ~120 for 32 compare/select pairs: this test runs on every pixel
+// that passes the compass pre-filter (k_level is VALU-issue bound).
 __device__ __forceinline__ bool fast_is_corner(const uint8_t* p, int TP, int t) {
-    const int v = p[0], hi = v + t, lo = v - t;
-    int c16[16];
-    c16[0] = p[3 * TP];
-    c16[1] = p[3 * TP + 1];
-    c16[2] = p[2 * TP + 2];
-    c16[3] = p[TP + 3];
-    c16[4] = p[3];
-    c16[5] = p[-TP + 3];
-    c16[6] = p[-2 * TP + 2];
-    c16[7] = p[-3 * TP + 1];
-    c16[8] = p[-3 * TP];
-    c16[9] = p[-3 * TP - 1];
-    c16[10] = p[-2 * TP - 2];
-    c16[11] = p[-TP - 3];
-    c16[12] = p[-3];
-    c16[13] = p[TP - 3];
-    c16[14] = p[2 * TP - 2];
-    c16[15] = p[3 * TP - 1];
-    uint32_t bri = 0, drk = 0;
+    const int v = p[0];
+    const uint32_t d0 = p[3 * TP] | (uint32_t)p[-3 * TP] << 16;           // c0,  c8
+    const uint32_t d1 = p[3 * TP + 1] | (uint32_t)p[-3 * TP - 1] << 16;   // c1,  c9
+    const uint32_t d2 = p[2 * TP + 2] | (uint32_t)p[-2 * TP - 2] << 16;   // c2,  c10
+    const uint32_t d3 = p[TP + 3] | (uint32_t)p[-TP - 3] << 16;           // c3,  c11
+    const uint32_t d4 = p[3] | (uint32_t)p[-3] << 16;                     // c4,  c12
+    const uint32_t d5 = p[-TP + 3] | (uint32_t)p[TP - 3] << 16;           // c5,  c13
+    const uint32_t d6 = p[-2 * TP + 2] | (uint32_t)p[2 * TP - 2] << 16;   // c6,  c14
+    const uint32_t d7 = p[-3 * TP + 1] | (uint32_t)p[3 * TP - 1] << 16;   // c7,  c15
+    const uint32_t d[8] = {d0, d1, d2, d3, d4, d5, d6, d7};
+    const short hi = (short)(v + t), lo = (short)(v - t);
+    const i16x2_t H = {hi, hi}, L = {lo, lo};
+    uint32_t mb = 0, md = 0;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        bri |= (uint32_t)(c16[k] > hi) << k;
-        drk |= (uint32_t)(c16[k] < lo) << k;
+    for (int k = 0; k < 8; ++k) {
+        const i16x2_t c = __builtin_bit_cast(i16x2_t, d[k]);
+        mb |= (__builtin_bit_cast(uint32_t, (i16x2_t)(H - c)) & 0x80008000u) >> k;
+        md |= (__builtin_bit_cast(uint32_t, (i16x2_t)(c - L)) & 0x80008000u) >> k;
     }
+    // flag k at bit 15 - k, flag k + 8 at bit 31 - k: bits 0..15 of (mb >> 24) | (mb & 0xFF00)
+    // run through flags 15..0, the circle in reverse cyclic order
+    const uint32_t bri = (mb >> 24) | (mb & 0xFF00u), drk = (md >> 24) | (md & 0xFF00u);
     auto has9 = [](uint32_t m) {
-        uint32_t m32 = m | (m << 16);
-        uint32_t a2 = m32 & (m32 >> 1);
-        uint32_t a4 = a2 & (a2 >> 2);
-        uint32_t a8 = a4 & (a4 >> 4);
+        const uint32_t m32 = m | (m << 16);
+        const uint32_t a2 = m32 & (m32 >> 1);
+        const uint32_t a4 = a2 & (a2 >> 2);
+        const uint32_t a8 = a4 & (a4 >> 4);
         return (a8 & (m32 >> 8) & 0xFFFFu) != 0;
     };
     return has9(bri) || has9(drk);
@@ -684,8 +687,11 @@ __device__ __forceinline__ int cell_of(const int* off, int n, int i) {
     return lo;
 }
 
+#ifndef KS_WAVES
+#define KS_WAVES 2  // waves per SIMD the register allocation targets
+#endif
 template <bool HARRIS>
-__global__ void __launch_bounds__(256) k_select(const uint8_t* __restrict__ pyr, uint32_t* __restrict__ cand,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAVES))) k_select(const uint8_t* __restrict__ pyr, uint32_t* __restrict__ cand,
                                                 uint32_t* __restrict__ cand2, int* __restrict__ cellCount, Geom g,
                                                 const CellGeom* __restrict__ cells, uint32_t* __restrict__ lvlOut,
                                                 int* __restrict__ lvlCount, uint64_t* __restrict__ candH,
