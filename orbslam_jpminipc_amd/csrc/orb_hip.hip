@@ -1014,8 +1014,11 @@ typedef short i16x2 __attribute__((ext_vector_type(2)));
 
 // Compass pre-filter of cv::FAST (a 9-arc always covers two cyclically adjacent points of
 // {0, 4, 8, 12}) for the 4 pixels of a dword, in packed 16-bit arithmetic: even and odd
-// bytes are split into u16 pairs; q > v + t <=> (v + t) - q < 0 and q < v - t <=> q - (v - t)
-// < 0 (all values within i16).  Returns a 4-bit mask (bit j = pixel j passes).
+// bytes are split into u16 pairs.  Bright: (q0 > v+t or q8 > v+t) and (q4 or q12 likewise)
+// <=> min(max(q0, q8), max(q4, q12)) > v + t; dark: max(min(q0, q8), min(q4, q12)) < v - t;
+// each comparison is the sign of an i16 difference (all values within i16).  Returns a 4-bit
+// mask (bit j = pixel j passes).
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t compass4(uint32_t c, uint32_t q0, uint32_t q4, uint32_t q8, uint32_t q12,
                                              uint32_t tt) {
     uint32_t pass[2];
@@ -1023,18 +1026,18 @@ __device__ __forceinline__ uint32_t compass4(uint32_t c, uint32_t q0, uint32_t q
     for (int h = 0; h < 2; ++h) {
         const uint32_t sel = h ? 0x0c030c01u : 0x0c020c00u;  // odd / even bytes -> u16 lanes
         const i16x2 v = __builtin_bit_cast(i16x2, __builtin_amdgcn_perm(0u, c, sel));
-        const i16x2 a = __builtin_bit_cast(i16x2, __builtin_amdgcn_perm(0u, q0, sel));
-        const i16x2 b = __builtin_bit_cast(i16x2, __builtin_amdgcn_perm(0u, q4, sel));
-        const i16x2 d = __builtin_bit_cast(i16x2, __builtin_amdgcn_perm(0u, q8, sel));
-        const i16x2 e = __builtin_bit_cast(i16x2, __builtin_amdgcn_perm(0u, q12, sel));
+        const u16x2 a = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(0u, q0, sel));
+        const u16x2 b = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(0u, q4, sel));
+        const u16x2 d = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(0u, q8, sel));
+        const u16x2 e = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(0u, q12, sel));
         const i16x2 t = __builtin_bit_cast(i16x2, tt);
-        const i16x2 hi = v + t, lo = v - t;
-        const uint32_t b0 = __builtin_bit_cast(uint32_t, (i16x2)(hi - a)), b4 = __builtin_bit_cast(uint32_t, (i16x2)(hi - b));
-        const uint32_t b8 = __builtin_bit_cast(uint32_t, (i16x2)(hi - d)), b12 = __builtin_bit_cast(uint32_t, (i16x2)(hi - e));
-        const uint32_t d0 = __builtin_bit_cast(uint32_t, (i16x2)(a - lo)), d4 = __builtin_bit_cast(uint32_t, (i16x2)(b - lo));
-        const uint32_t d8 = __builtin_bit_cast(uint32_t, (i16x2)(d - lo)), d12 = __builtin_bit_cast(uint32_t, (i16x2)(e - lo));
-        // some cyclically adjacent pair of {0,4,8,12}: (m0 | m8) & (m4 | m12)
-        pass[h] = (((b0 | b8) & (b4 | b12)) | ((d0 | d8) & (d4 | d12))) & 0x80008000u;
+        const i16x2 M = __builtin_bit_cast(
+            i16x2, __builtin_elementwise_min(__builtin_elementwise_max(a, d), __builtin_elementwise_max(b, e)));
+        const i16x2 m = __builtin_bit_cast(
+            i16x2, __builtin_elementwise_max(__builtin_elementwise_min(a, d), __builtin_elementwise_min(b, e)));
+        const uint32_t br = __builtin_bit_cast(uint32_t, (i16x2)((v + t) - M));  // < 0: bright
+        const uint32_t dk = __builtin_bit_cast(uint32_t, (i16x2)(m - (v - t)));  // < 0: dark
+        pass[h] = (br | dk) & 0x80008000u;
     }
     // bit 15 / 31 of even -> pixels 0 / 2, of odd -> pixels 1 / 3
     return ((pass[0] >> 15) & 1u) | ((pass[1] >> 14) & 2u) | ((pass[0] >> 29) & 4u) | ((pass[1] >> 28) & 8u);
