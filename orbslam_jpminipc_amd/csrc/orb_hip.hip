@@ -129,6 +129,9 @@ __constant__ signed char c_pattern[1024];
 #ifndef KL_COUNT
 #define KL_COUNT 0
 #endif
+#ifndef KL_SKIP_THIN  // timing experiment only: drop tiles with < 64 live columns (wrong output)
+#define KL_SKIP_THIN 0
+#endif
 #if KL_COUNT
 __device__ unsigned long long g_klcount[4];  // lane-rows queued, pixels expanded, corners, survivors
 #endif
@@ -1494,6 +1497,12 @@ struct MatchGeom {
 //            if a truncated top-8 holds < 2 such candidates the wave rescans the window.
 //   phase 3  rotation histogram, ComputeThreeMaxima, vnMatches12 / vbPrevMatched out.
 #define MATCH_TOPK 8
+#ifndef KM_SKIP1  // timing experiments only (wrong output): skip the phase-1 scan / phase 2
+#define KM_SKIP1 0
+#endif
+#ifndef KM_SKIP2
+#define KM_SKIP2 0
+#endif
 __device__ __forceinline__ void topk_insert(uint32_t (&t)[MATCH_TOPK], uint32_t key) {
 #pragma unroll
     for (int i = 0; i < MATCH_TOPK; ++i) {
@@ -1513,6 +1522,7 @@ __global__ void __launch_bounds__(256) k_match_init(const orb_keypoint_t* __rest
     __shared__ int s_n2c, s_n1c;
     __shared__ int s_hist[32];
     __shared__ int s_ind[3];
+    __shared__ int s_col[65];  // first slot of grid column cx (slots are in (cx, cy, index) order)
     const int p = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int f1 = pf1[p], f2 = pf2[p];
     const int n1 = counts[f1], n2 = counts[f2];
@@ -1602,6 +1612,17 @@ __global__ void __launch_bounds__(256) k_match_init(const orb_keypoint_t* __rest
         s_m12[i] = -1;
         s_bslot[i] = -1;
     }
+    if (tid <= 64) {  // lower_bound(s_cell, tid * 48): a window's columns are one slot range
+        int lo = 0, hi = n2c;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (s_cell[mid] < tid * 48)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        s_col[tid] = lo;
+    }
     __syncthreads();
     // ---- phase 1: per-query top-8 (dist, order) ----
     for (int q0 = 0; q0 < n1c; q0 += 256) {
@@ -1625,7 +1646,9 @@ __global__ void __launch_bounds__(256) k_match_init(const orb_keypoint_t* __rest
 #pragma unroll
         for (int k = 0; k < MATCH_TOPK; ++k) top[k] = 0xFFFFFFFFu;
         int cnt = 0;
-        for (int j = 0; j < n2c; ++j) {  // uniform j: LDS broadcast reads
+        // the window's grid columns only (an empty column range gives j0 >= j1)
+        const int j0 = s_col[min(minCX, 64)], j1 = KM_SKIP1 ? 0 : s_col[max(maxCX + 1, 0)];
+        for (int j = j0; j < j1; ++j) {
             const int cell = s_cell[j];
             const int cx = cell / 48, cy = cell - cx * 48;
             if (cx < minCX || cx > maxCX || cy < minCY || cy > maxCY) continue;
@@ -1645,7 +1668,7 @@ __global__ void __launch_bounds__(256) k_match_init(const orb_keypoint_t* __rest
     // Per query the critical path is one LDS read of its top-8 slots' state and scalar lane
     // reads (v_readlane: no LDS round trip); the next query's list is fetched while this one
     // resolves, and the rotation bins are computed afterwards, in parallel (phase 3).
-    if (wave == 0 && n1c > 0) {
+    if (wave == 0 && n1c > 0 && !KM_SKIP2) {
         int cntN = s_lcnt[0], i1N = s_q2i[0];
         uint32_t eN = lane < MATCH_TOPK ? s_list[lane] : 0xFFFFFFFFu;
         for (int q = 0; q < n1c; ++q) {
@@ -1684,7 +1707,8 @@ __global__ void __launch_bounds__(256) k_match_init(const orb_keypoint_t* __rest
                 for (int w = 0; w < 8; ++w) d1[w] = D1[(long long)i1 * 8 + w];
                 uint32_t lb = 0xFFFFFFFFu;
                 int ls = 0x7fffffff;
-                for (int j = lane; j < n2c; j += 64) {
+                const int j1 = s_col[max(maxCX + 1, 0)];
+                for (int j = s_col[min(minCX, 64)] + lane; j < j1; j += 64) {
                     const int cell = s_cell[j];
                     const int cx = cell / 48, cy = cell - cx * 48;
                     if (cx < minCX || cx > maxCX || cy < minCY || cy > maxCY) continue;
@@ -2156,7 +2180,8 @@ struct orb_extractor {
         std::vector<BlurTile> tl;
         for (int l = 0; l < nlevels; ++l)
             for (int y0 = -3; y0 < G.lv[l].ringY1; y0 += BLUR_TH)
-                for (int x0 = -4; x0 < G.lv[l].ringX1; x0 += BLUR_TW) tl.push_back(BlurTile{l, x0, y0});
+                for (int x0 = -4; x0 < G.lv[l].ringX1; x0 += BLUR_TW)
+                    if (!KL_SKIP_THIN || G.lv[l].ringX1 - x0 >= 64) tl.push_back(BlurTile{l, x0, y0});
         HIP_TRY(hipMalloc(&d_tiles, tl.size() * sizeof(BlurTile)));
         HIP_TRY(hipMemcpy(d_tiles, tl.data(), tl.size() * sizeof(BlurTile), hipMemcpyHostToDevice));
         nTiles = (int)tl.size();
