@@ -412,6 +412,109 @@ __global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, c
     }
 }
 
+// Levels lf .. L-1 of one frame per 1024-thread workgroup (the small levels: one launch
+// instead of one per level, each of which was latency-bound at a few thousand pixels per
+// frame).  Level lf reads level lf-1 from HBM; every later level reads its source ROI from
+// LDS, where the previous level left it (ping-pong buffers A / B); the level's resize tables
+// are staged in LDS too.  Per padded pixel the arithmetic is k_pyr_resize's: HResizeLinear
+// taps (tail columns S[sx] * 2048), then the SSE2 vertical body (((H >> 4) * b) >> 16 summed,
+// + 2 >> 2) on columns lx < xs, the scalar FixedPtCast (+ 2^21 >> 22) on the others.
+#define RT_THREADS 1024
+#define RT_LDS_MAX (150 * 1024)
+#ifndef KR_TAIL  // 0: every level by k_pyr_resize (experiment switch)
+#define KR_TAIL 1
+#endif
+__global__ void __launch_bounds__(RT_THREADS) k_pyr_resize_tail(uint8_t* __restrict__ pyr,
+                                                                const int* __restrict__ rtab, Geom g, int lf,
+                                                                int bufA, int bufB) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_rt[];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    int* tab = (int*)(s_rt + bufA + bufB);
+    for (int l = lf; l < g.L; ++l) {
+        const LevelGeom lg = g.lv[l], ls = g.lv[l - 1];
+        const int w = lg.w, h = lg.h, sw = ls.w, sh = ls.h;
+        const int* src = rtab + lg.rtab;
+        for (int i = tid; i < 2 * (w + h); i += RT_THREADS) tab[i] = src[i];
+        __syncthreads();
+        const int *xofs = tab, *alpha = tab + w, *yofs = tab + 2 * w, *beta = yofs + h;
+        const uint8_t* Sg = pyr + ls.base + (long long)b * ls.fstride + (long long)EDGE * ls.pitch + EDGE;
+        // level l-lf even -> buffer A at 0, odd -> buffer B at bufA (bufB: B's size)
+        const uint8_t* Sl = s_rt + (((l - 1 - lf) & 1) ? bufA : 0);  // level l-1's ROI (l > lf)
+        uint8_t* Dl = (l + 1 < g.L) ? s_rt + (((l - lf) & 1) ? bufA : 0) : nullptr;
+        const long long spitch = l > lf ? sw : ls.pitch;
+        const uint8_t* S = l > lf ? Sl : Sg;
+        uint8_t* D = pyr + lg.base + (long long)b * lg.fstride;
+        const int nw = lg.pitch >> 2, rowsPerPass = RT_THREADS / nw;
+        const int r0 = tid / nw, c4 = (tid - r0 * nw) * 4;
+        if (r0 < rowsPerPass) {
+            int sx[4], sx1[4];
+            uint32_t a0[4], a1[4];
+            bool simd[4], live[4], roiX[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int px = c4 + j;
+                live[j] = px < w + 2 * EDGE;
+                roiX[j] = px >= EDGE && px < EDGE + w;
+                const int lx = reflect101(min(px, w + 2 * EDGE - 1) - EDGE, w);
+                sx[j] = xofs[lx];
+                if (lx < lg.xmax) {
+                    const int aa = alpha[lx];
+                    a0[j] = (uint32_t)(aa & 0xFFFF);
+                    a1[j] = (uint32_t)(aa >> 16) & 0xFFFFu;
+                } else {
+                    a0[j] = 2048;
+                    a1[j] = 0;
+                }
+                sx1[j] = a1[j] ? sx[j] + 1 : sx[j];
+                simd[j] = lx < lg.xs_resize;
+            }
+            // four rows per step, all their source bytes loaded before any is used: the first
+            // fused level reads HBM / L2, and a thread's rows would otherwise be one exposed
+            // round trip each
+            for (int py0 = r0; py0 < lg.ph; py0 += 4 * rowsPerPass) {
+                uint32_t v[4][4][4];
+                uint32_t bk[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int py = min(py0 + k * rowsPerPass, lg.ph - 1);
+                    const int ly = reflect101(py - EDGE, h);
+                    const int sy = yofs[ly];
+                    bk[k] = (uint32_t)beta[ly];
+                    const uint8_t* R0 = S + min(max(sy, 0), sh - 1) * spitch;
+                    const uint8_t* R1 = S + min(max(sy + 1, 0), sh - 1) * spitch;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        v[k][j][0] = R0[sx[j]];
+                        v[k][j][1] = R0[sx1[j]];
+                        v[k][j][2] = R1[sx[j]];
+                        v[k][j][3] = R1[sx1[j]];
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int py = py0 + k * rowsPerPass;
+                    if (py >= lg.ph) break;
+                    const uint32_t b0 = bk[k] & 0xFFFFu, b1 = bk[k] >> 16;
+                    const bool roiY = Dl && py >= EDGE && py < EDGE + h;
+                    uint32_t word = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const uint32_t hA = v[k][j][0] * a0[j] + v[k][j][1] * a1[j];
+                        const uint32_t hB = v[k][j][2] * a0[j] + v[k][j][3] * a1[j];
+                        const uint32_t r = simd[j]
+                                               ? (__umulhi(hA >> 4, b0 << 16) + __umulhi(hB >> 4, b1 << 16) + 2u) >> 2
+                                               : (hA * b0 + hB * b1 + (1u << 21)) >> 22;
+                        if (live[j]) word |= r << (8 * j);
+                        if (roiY && roiX[j]) Dl[(py - EDGE) * w + (c4 + j - EDGE)] = (uint8_t)r;
+                    }
+                    *(uint32_t*)(D + (long long)py * lg.pitch + c4) = word;
+                }
+            }
+        }
+        __syncthreads();  // level l complete in LDS; the tables are free
+    }
+}
+
 // ---- FAST per cell ----------------------------------------------------------------------
 // One workgroup (4 waves) per (cell, frame); the cell ROI (cell + 3 px each side) is staged
 // in LDS.  For threshold t = fastTh (and again at t = 7 when that finds <= 3 corners,
@@ -1867,6 +1970,9 @@ struct orb_extractor {
     std::vector<int> rtab;
     size_t cellLds = 0, selectLds = 0;
     size_t resizeLds[ORB_MAX_LEVELS] = {};
+    int resizeTail = 0;           // first level of k_pyr_resize_tail (nlevels: none)
+    int tailBufA = 0, tailBufB = 0;
+    size_t tailLds = 0;
     // device workspace
     uint8_t* d_pyr = nullptr;
     uint8_t* d_blur = nullptr;
@@ -2171,6 +2277,21 @@ struct orb_extractor {
             if (lds > 96 * 1024) return set_err(ORB_ENOTSUP, "scale factor too large for the resize tile");
             resizeLds[l] = lds;
         }
+        // the fused small-level tail: the first level from which every later level's source
+        // ROI (ping-pong A / B) plus the staged tables fit the CU's LDS
+        resizeTail = nlevels;
+        for (int l = 1; l + 1 < nlevels; ++l) {
+            auto roi = [&](int k) { return k + 1 < nlevels ? (size_t)G.lv[k].w * G.lv[k].h : (size_t)0; };
+            const size_t a = (roi(l) + 15) & ~(size_t)15, bsz = (roi(l + 1) + 15) & ~(size_t)15;
+            const size_t need = a + bsz + (size_t)8 * (G.lv[l].w + G.lv[l].h);
+            if (need <= (size_t)RT_LDS_MAX && KR_TAIL) {
+                resizeTail = l;
+                tailBufA = (int)a;
+                tailBufB = (int)bsz;
+                tailLds = need;
+                break;
+            }
+        }
         G.nCells = (int)cl.size();
         G.candPerFrame = cand;
         G.kpCap = kpCap;
@@ -2267,11 +2388,14 @@ struct orb_extractor {
         }
         stage_end(0, st);
         stage_begin(1, st);
-        for (int l = 1; l < nlevels; ++l) {
+        for (int l = 1; l < resizeTail; ++l) {
             const LevelGeom& lg = g.lv[l];
             dim3 grid((lg.pitch + RZ_TW - 1) / RZ_TW, (lg.ph + RZ_TH - 1) / RZ_TH, B);
             hipLaunchKernelGGL(k_pyr_resize, grid, dim3(256), resizeLds[l], st, d_pyr, d_rtab, g.lv[l], g.lv[l - 1]);
         }
+        if (resizeTail < nlevels)
+            hipLaunchKernelGGL(k_pyr_resize_tail, dim3(B), dim3(RT_THREADS), tailLds, st, d_pyr, d_rtab, g, resizeTail,
+                               tailBufA, tailBufB);
         stage_end(1, st);
         stage_begin(2, st);
         HIP_TRY(hipMemsetAsync(d_cellCount, 0, (size_t)g.nCells * B * 4, st));
@@ -2331,6 +2455,7 @@ int orb_extractor_create(int nfeatures, float scale_factor, int nlevels, int sco
     if (st) return st;
     // k_select<true> (HARRIS_SCORE) stages (response, record) pairs: up to 96 KB of LDS
     hipFuncSetAttribute((const void*)k_select<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    hipFuncSetAttribute((const void*)k_pyr_resize_tail, hipFuncAttributeMaxDynamicSharedMemorySize, RT_LDS_MAX);
     orb_extractor* h = new orb_extractor();
     h->nfeatures = nfeatures;
     h->scaleFactor = scale_factor;
