@@ -126,6 +126,7 @@ struct CellGeom {
 using namespace orbdev;
 
 __constant__ signed char c_pattern[1024];
+__constant__ float c_patternf[1024];  // the same pattern as floats: lane l's 8 points are 4 float4
 #ifndef KL_COUNT
 #define KL_COUNT 0
 #endif
@@ -1465,7 +1466,9 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
         if (k >= g.lv[i].kpBase) l = i;
     const LevelGeom& lg = g.lv[l];
     const int idx = k - lg.kpBase;
-    const uint32_t e = k < g.kpCap ? lvlOut[(long long)b * g.kpCap + k] : 0u;
+    // wave-uniform record: x, y and the patch bases below live in SGPRs, so every patch load
+    // is SGPR base + 32-bit lane offset (no 64-bit address arithmetic per load)
+    const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane((int)(k < g.kpCap ? lvlOut[(long long)b * g.kpCap + k] : 0u));
     // output position: level-major order (ORBextractor.cc:749-778)
     int before = 0, cntL = 0, total = 0;
     for (int i = 0; i < g.L; ++i) {
@@ -1482,35 +1485,37 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
     // raw 31x31 patch, rows y-15..y+15, cols x-15..x+15 (dword-aligned spans)
     const uint8_t* p0 = pyr + fbase + (long long)(y + EDGE - HALF_PATCH) * lg.pitch + (x + EDGE - HALF_PATCH);
     const int sh = (int)((uintptr_t)p0 & 3);
-    const uint32_t* w0 = (const uint32_t*)(p0 - sh);
+    const uint8_t* w0 = p0 - sh;
     // descriptor window, rows y-18..y+18, cols x-18..x+18 (inside the padded level: x, y lie in
     // the detection region and ringX1/Y1 <= w/h + 12)
     const uint8_t* q0 = blur + fbase + (long long)(y + EDGE - DW_R) * lg.pitch + (x + EDGE - DW_R);
     const int wsh = (int)((uintptr_t)q0 & 3);
-    const uint32_t* v0 = (const uint32_t*)(q0 - wsh);
+    const uint8_t* v0 = q0 - wsh;
     uint32_t* P = s_patch[wave];
     uint32_t* Q = s_win[wave];
     constexpr int NP = (31 * 9 + 63) / 64, NW = ((2 * DW_R + 1) * 10 + 63) / 64;
+    const uint32_t pitch = (uint32_t)lg.pitch;
     uint32_t pv[NP], wv[NW];
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
-        const int i = lane + 64 * j, r = i / 9, c = i - r * 9;
-        pv[j] = i < 31 * 9 ? w0[(long long)r * spw + c] : 0u;
+        const int i = lane + 64 * j, r = i / 9, c = i - __mul24(r, 9);
+        pv[j] = i < 31 * 9 ? *(const uint32_t*)(w0 + (__umul24((uint32_t)r, pitch) + 4u * c)) : 0u;
     }
 #pragma unroll
     for (int j = 0; j < NW; ++j) {
-        const int i = lane + 64 * j, r = i / 10, c = i - r * 10;
-        wv[j] = i < (2 * DW_R + 1) * 10 ? v0[(long long)r * spw + c] : 0u;
+        const int i = lane + 64 * j, r = i / 10, c = i - __mul24(r, 10);
+        wv[j] = i < (2 * DW_R + 1) * 10 ? *(const uint32_t*)(v0 + (__umul24((uint32_t)r, pitch) + 4u * c)) : 0u;
     }
+    // LDS rows of 9 (patch) and 10 (window) dwords: the LDS index is the load index itself
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
-        const int i = lane + 64 * j, r = i / 9, c = i - r * 9;
-        if (i < 31 * 9) P[r * (IC_P / 4) + c] = pv[j];
+        const int i = lane + 64 * j;
+        if (i < 31 * 9) P[i] = pv[j];
     }
 #pragma unroll
     for (int j = 0; j < NW; ++j) {
-        const int i = lane + 64 * j, r = i / 10, c = i - r * 10;
-        if (i < (2 * DW_R + 1) * 10) Q[r * (DW_P / 4) + c] = wv[j];
+        const int i = lane + 64 * j;
+        if (i < (2 * DW_R + 1) * 10) Q[i] = wv[j];
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS is in order per wave; compiler fence
     // IC_Angle (ORBextractor.cc:124-151): the disc sums m10 = sum u*I, m01 = sum v*I over
@@ -1536,8 +1541,8 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
                 const uint32_t pm = P[n] & mask;
                 const int S = (int)__builtin_amdgcn_udot4(pm, 0x01010101u, 0u, false);
                 const int T = (int)__builtin_amdgcn_udot4(pm, 0x03020100u, 0u, false);
-                m10 += base * S + T;
-                m01 += v * S;
+                m10 += __mul24(base, S) + T;  // 24-bit multiplies: full-rate VALU
+                m01 += __mul24(v, S);
             }
         }
     }
@@ -1554,13 +1559,21 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
     const float a = ca, bsin = sa;
     const uint8_t* center = (const uint8_t*)Q + wsh + DW_R * DW_P + DW_R;
     int vals[8];
+    float pat[16];  // pattern points 8*lane .. 8*lane+7 (tests 4*lane .. 4*lane+3): 4 float4 loads
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const float4 f = ((const float4*)c_patternf)[lane * 4 + q];
+        pat[4 * q] = f.x;
+        pat[4 * q + 1] = f.y;
+        pat[4 * q + 2] = f.z;
+        pat[4 * q + 3] = f.w;
+    }
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-        const int pt = lane * 8 + q;  // pattern point: tests 4*lane .. 4*lane+3
-        const float px = (float)c_pattern[2 * pt], py = (float)c_pattern[2 * pt + 1];
+        const float px = pat[2 * q], py = pat[2 * q + 1];
         const int dy = (int)rintf(__builtin_fmaf(px, bsin, py * a));
         const int dx = (int)rintf(__builtin_fmaf(px, a, -(py * bsin)));
-        vals[q] = center[dy * DW_P + dx];
+        vals[q] = center[__mul24(dy, DW_P) + dx];
     }
     int nib = 0;
 #pragma unroll
@@ -2426,6 +2439,9 @@ static int upload_pattern(int device) {
     std::lock_guard<std::mutex> lock(mu);
     if (device >= 0 && device < 64 && uploaded[device]) return ORB_OK;
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), kOrbPattern31, sizeof(kOrbPattern31)));
+    float pf[1024];
+    for (int i = 0; i < 1024; ++i) pf[i] = (float)kOrbPattern31[i];
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_patternf), pf, sizeof(pf)));
     if (device >= 0 && device < 64) uploaded[device] = true;
     return ORB_OK;
 }
