@@ -1085,7 +1085,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
 // SymmColumnVec_32s8u float path), the tail columns half-up ((T + 2^15) >> 16).
 #define BLUR_TW 256  // output columns per tile: 64 lanes x 4 pixels
 #ifndef BLUR_RW
-#define BLUR_RW 12   // output rows per wave (48-row tiles: ~39 KB LDS, 4 work-groups per CU)
+#define BLUR_RW 9    // output rows per wave: 36-row tiles, 31.5 KB LDS, 5 work-groups per CU (87 VGPRs).
+                     // Measured (640x480, B=256): 8 rows 826 us, 9 rows 734, 12 rows 750.
 #endif
 #define BLUR_TH (4 * BLUR_RW)  // output rows per tile (4 waves)
 #define BLUR_IW 66   // LDS row pitch in dwords: tile columns x0-4 .. x0+259
