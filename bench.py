@@ -74,17 +74,18 @@ def stage_bytes(W, H, n_kp, n_cand, n_pairs_kp0, B):
 def pmc_traffic(kernel, W, H, B, NF):
     """HBM bytes per launch of `kernel` from the committed PMC summary of this workload
     (profiles/pmc_latest.json, written by scripts/pmc_summary.py from rocprofv3 FETCH_SIZE /
-    WRITE_SIZE passes over bench.py), or (None, None) when it does not cover this run."""
+    WRITE_SIZE passes over bench.py) with the source tag and the kernel's SQ_INSTS_VALU (wave
+    instructions per launch), or Nones when the summary does not cover this run."""
     try:
         with open(os.path.join(ROOT, "profiles", "pmc_latest.json")) as f:
             d = json.load(f)
     except (OSError, ValueError):
-        return None, None
+        return None, None, None
     w = d.get("workload", {})
     if (w.get("width"), w.get("height"), w.get("batch"), w.get("nfeatures")) != (W, H, B, NF):
-        return None, None
+        return None, None, None
     k = d.get("per_launch", {}).get(kernel)
-    return (k["hbm_bytes"], d.get("source")) if k else (None, None)
+    return (k["hbm_bytes"], d.get("source"), k.get("SQ_INSTS_VALU")) if k else (None, None, None)
 
 
 def cpu_baseline(frames, nfeatures, threads, W, H):
@@ -275,17 +276,22 @@ def main():
             "GBps": nbytes / (per_launch_ms * 1e-3) / 1e9 if per_launch_ms > 0 else None,
             "measured_in": "timed region" if name == dom else "survey pass",
         }
-    # the resize stage launches one kernel per level: report per-kernel-launch numbers
+    # the resize stage builds levels 1-7 (k_pyr_resize per large level, the small levels in one
+    # k_pyr_resize_tail launch): report per-level numbers
     if "k_pyr_resize" in stages:
         s = stages["k_pyr_resize"]
         s["launches"] *= 7
         s["ms_per_launch"] /= 7
         s["GBps"] = s["bytes_per_launch"] / (s["ms_per_launch"] * 1e-3) / 1e9
+        s["note"] = "per pyramid level (levels 1-7; the small levels share one k_pyr_resize_tail launch)"
     ds = stages[dom]
     per_step_s = tmax / args.steps
 
     value = replicas.whole_job_rate(B * args.steps, world, tmax)
-    traffic, traffic_src = pmc_traffic(dom, W, H, B, NF)
+    traffic, traffic_src, valu_insts = pmc_traffic(dom, W, H, B, NF)
+    # VALU issue ceiling: each SIMD issues one wave64 VALU instruction per 2 cycles
+    # (MI355X_MICROARCH.md), 4 SIMDs x 256 CUs at 2.4 GHz
+    valu_peak = 256 * 4 / 2 * 2.4e9
     result = {
         "metric": "frames/sec ORB extract+match, 640x480 8-level 1000 kp; HBM GB/s vs peak",
         "value": value,
@@ -320,6 +326,8 @@ def main():
             "traffic_unit": "bytes per launch (rocprofv3 PMC)",
             "traffic_source": traffic_src,
             "algorithmic_bytes_per_launch": ds["bytes_per_launch"],
+            "valu_insts_per_launch": valu_insts,
+            "valu_issue_frac": (valu_insts / (ds["ms_per_launch"] * 1e-3) / valu_peak) if valu_insts else None,
         },
         "pipeline": {
             "algorithmic_bytes_per_step": b_ext + b_match,
