@@ -634,11 +634,42 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
         for (int i = tid; i < nw; i += 256) ((uint32_t*)Fl)[i] = 0u;
     }
     __syncthreads();
-    for (int yy = wave; yy < dh; yy += 4)
-        for (int xx = lane; xx < dw; xx += 64) {
-            const uint8_t* p = In + (yy + 3) * inW + xx + 3 + o;
-            Sp[yy * dwp + xx] = fast_is_corner(p, inW, t) ? (uint8_t)fast_exact_strength(p, inW) : (uint8_t)0;
+    // corner test per pixel; corners queued per wave and their exact strengths computed 64 at
+    // a time with every lane busy (textured cells have corners in most 64-pixel chunks)
+    {
+        uint32_t* rq = (uint32_t*)(In + (((size_t)inW * (dh + 6) + 3) & ~(size_t)3)) + wave * 128;
+        const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+        int pn = 0;
+        auto flush64 = [&]() {  // strengths of rq[0..63], then the rest moves to the front
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            const uint32_t q = rq[lane];
+            const int qy = (int)(q >> 16), qx = (int)(q & 0xFFFFu);
+            Sp[qy * dwp + qx] = (uint8_t)fast_exact_strength(In + (qy + 3) * inW + qx + 3 + o, inW);
+            const uint32_t r = 64 + lane < pn ? rq[64 + lane] : 0u;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (64 + lane < pn) rq[lane] = r;
+            pn -= 64;
+        };
+        for (int yy = wave; yy < dh; yy += 4)
+            for (int xx0 = 0; xx0 < dw; xx0 += 64) {
+                const int xx = xx0 + lane;
+                bool corner = false;
+                if (xx < dw) {
+                    corner = fast_is_corner(In + (yy + 3) * inW + xx + 3 + o, inW, t);
+                    Sp[yy * dwp + xx] = 0;
+                }
+                const uint64_t m = __ballot(corner);
+                if (corner) rq[pn + __popcll(m & below)] = ((uint32_t)yy << 16) | (uint32_t)xx;
+                pn += __popcll(m);
+                if (pn >= 64) flush64();
+            }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane < pn) {
+            const uint32_t q = rq[lane];
+            const int qy = (int)(q >> 16), qx = (int)(q & 0xFFFFu);
+            Sp[qy * dwp + qx] = (uint8_t)fast_exact_strength(In + (qy + 3) * inW + qx + 3 + o, inW);
         }
+    }
     __syncthreads();
     for (int yy = wave; yy < dh; yy += 4)
         for (int xx = lane; xx < dw; xx += 64) {
@@ -2196,7 +2227,7 @@ struct orb_extractor {
                             const size_t dwp = (size_t)((std::max(dw, 0) + 3) & ~3);
                             const size_t inW = (size_t)((3 + std::max(dw, 0) + 6 + 3) & ~3);
                             size_t lds = 2 * dwp * std::max(dh, 0) + 4 * (size_t)((std::max(dh, 0) + 3) & ~3) +
-                                         inW * (std::max(dh, 0) + 6) + 16;
+                                         inW * (std::max(dh, 0) + 6) + 16 + 4 * 4 * 128;  // + corner queues
                             cellLds = std::max(cellLds, lds);
                         }
                     }
