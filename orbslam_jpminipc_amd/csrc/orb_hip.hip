@@ -671,31 +671,32 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
         }
     }
     __syncthreads();
-    for (int yy = wave; yy < dh; yy += 4)
-        for (int xx = lane; xx < dw; xx += 64) {
-            const int s0 = Sp[yy * dwp + xx];
-            if (s0 <= t) continue;
-            bool keep = true;
-#pragma unroll
-            for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-                for (int dx = -1; dx <= 1; ++dx) {
-                    if (dx == 0 && dy == 0) continue;
-                    const int nx = xx + dx, ny = yy + dy;
-                    const int n = (nx >= 0 && nx < dw && ny >= 0 && ny < dh) ? Sp[ny * dwp + nx] : 0;
-                    keep = keep && (s0 - 1 > (n > t ? n - 1 : 0));
-                }
-            if (keep) Fl[yy * dwp + xx] = 1;
-        }
-    __syncthreads();
-    // raster-order compaction from the flag plane: row counts, scan, write
+    // 3x3 NMS; each row's survivor count comes from the same ballots (no second pass)
     const uint32_t* Flw = (const uint32_t*)Fl;
     for (int yy = wave; yy < dh; yy += 4) {
-        int cnt = 0;
-        for (int w = lane; w < rw; w += 64) cnt += __popc(Flw[yy * rw + w]);
+        int rc = 0;
+        for (int xx0 = 0; xx0 < dw; xx0 += 64) {
+            const int xx = xx0 + lane;
+            bool keep = false;
+            if (xx < dw) {
+                const int s0 = Sp[yy * dwp + xx];
+                if (s0 > t) {
+                    keep = true;
 #pragma unroll
-        for (int o2 = 32; o2 >= 1; o2 >>= 1) cnt += __shfl_xor(cnt, o2, 64);
-        if (lane == 0) rowc[yy] = cnt;
+                    for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+                        for (int dx = -1; dx <= 1; ++dx) {
+                            if (dx == 0 && dy == 0) continue;
+                            const int nx = xx + dx, ny = yy + dy;
+                            const int n = (nx >= 0 && nx < dw && ny >= 0 && ny < dh) ? Sp[ny * dwp + nx] : 0;
+                            keep = keep && (s0 - 1 > (n > t ? n - 1 : 0));
+                        }
+                }
+            }
+            if (keep) Fl[yy * dwp + xx] = 1;
+            rc += __popcll(__ballot(keep));
+        }
+        if (lane == 0) rowc[yy] = rc;
     }
     __syncthreads();
     __shared__ int s_total;
