@@ -629,8 +629,9 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
     {
         const uint32_t* src = (const uint32_t*)(det - 3 * (long long)pitch - 3 - o);
         const int nwr = inW >> 2, pw = pitch >> 2;
-        for (int r = wave; r < dh + 6; r += 4)
-            for (int k = lane; k < nwr; k += 64) ((uint32_t*)In)[r * nwr + k] = src[(long long)r * pw + k];
+        // all loads of a batch in flight before any LDS write (one round trip per 20 dwords
+        // per thread, instead of one per row group)
+        stage_rows_to_lds((uint32_t*)In, nwr, src, pw, dh + 6, nwr, nwr, tid);
         for (int i = tid; i < nw; i += 256) ((uint32_t*)Fl)[i] = 0u;
     }
     __syncthreads();
