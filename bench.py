@@ -120,7 +120,8 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=3072,
                     help="CPU-baseline sample size (0 = skip); ~20 s of CPU-thread time on 16 threads")
     ap.add_argument("--overlap", type=int, default=0,
-                    help="1: extract(t) on one stream while matching batch t-1 on another; 0: serial step")
+                    help="1: extract(t) on one stream while matching batch t-1 on another; 2: only the "
+                         "pyramid of batch t overlaps the matching of batch t-1; 0: serial step")
     ap.add_argument("--survey-steps", type=int, default=5, help="untimed steps with every stage bracketed")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = OMP_NUM_THREADS or os.cpu_count()")
     args = ap.parse_args()
@@ -177,6 +178,25 @@ def main():
         t = st["t"]
         st["t"] += 1
         cur, prev = t % 2, (t - 1) % 2
+        if st["overlap"] == 2:
+            # pyramid(t) || match(t-1); detection..descriptors of t after match(t-1), so the
+            # matcher's LDS-heavy work-groups never share the chip with k_level's
+            with torch.cuda.stream(s_ext):
+                ext.set_phases(1)
+                ext.extract_batch_device(d_imgs, *bufs[cur], stream=s_ext)
+            nm = None
+            if t >= 1:
+                with torch.cuda.stream(s_match):
+                    s_match.wait_event(ev_edone[prev])
+                    nm = match(*bufs[prev], s_match, timed)
+                    ev_mdone[prev].record(s_match)
+                s_ext.wait_event(ev_mdone[prev])  # also: match(t-2) has read bufs[cur]
+            with torch.cuda.stream(s_ext):
+                ext.set_phases(2)
+                ext.extract_batch_device(d_imgs, *bufs[cur], stream=s_ext)
+                ext.set_phases(3)
+                ev_edone[cur].record(s_ext)
+            return nm
         with torch.cuda.stream(s_ext):
             if t >= 2:
                 s_ext.wait_event(ev_mdone[cur])  # match(t-2) has read this buffer
@@ -311,8 +331,10 @@ def main():
             "batch_per_gpu": B,
             "pairs_per_gpu": B - 1,
             "parallelism": f"replicas x{world} (no collectives)",
-            "streams": "extract(t) || SearchForInitialization(t-1), double-buffered" if args.overlap
-                       else "one stream, extract then match",
+            "streams": {0: "one stream, extract then match",
+                        1: "extract(t) || SearchForInitialization(t-1), double-buffered",
+                        2: "pyramid(t) || SearchForInitialization(t-1), then the rest of extract(t)"}
+                       [args.overlap],
         },
 
         "roofline": {

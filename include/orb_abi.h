@@ -387,6 +387,15 @@ int orb_profile_enable_stages(orb_extractor_t* h, unsigned stage_mask);
 int orb_profile_read(orb_extractor_t* h, double* stage_ms, int64_t* stage_launches, int nstages);
 const char* orb_profile_stage_name(int i);
 
+/* Split orb_extract_batch_device into its two phases (scheduling only; results unchanged):
+ * bit 0 = the image pyramid (ORBextractor.cc:1086-1117 ComputePyramid), bit 1 = detection,
+ * selection, orientation and descriptors (ComputeKeyPointsOctTree + the descriptor loop,
+ * ORBextractor.cc:578-708, 749-778), which read the pyramid that bit 0 left in the extractor's
+ * workspace.  A caller running phase 1 then phase 2 for the same batch, on one stream or
+ * event-ordered, gets exactly the mask-3 result; the gap between them lets other work (the
+ * previous batch's matching) overlap the pyramid.  Default 3.  No reference counterpart. */
+int orb_extract_set_phases(orb_extractor_t* h, unsigned phase_mask);
+
 /* ---- test hooks (no device work unless stated) ------------------------------------- */
 /* Host instantiation of the kernels' libstdc++ nth_element replay on packed u32 elements
  * (score in bits 24..31), for CPU unit tests against std::nth_element. */

@@ -165,6 +165,7 @@ HIP_SIGNATURES = {
     "orb_vocabulary_transform": (_i, [_vp, _vp, _i, _i, _vp, _vp, _pi, _vp, _vp, _vp, _pi]),
     "orb_profile_enable": (_i, [_vp, _i]),
     "orb_profile_enable_stages": (_i, [_vp, ctypes.c_uint]),
+    "orb_extract_set_phases": (_i, [_vp, ctypes.c_uint]),
     "orb_profile_read": (_i, [_vp, _vp, _vp, _i]),
     "orb_profile_stage_name": (ctypes.c_char_p, [_i]),
     "orb_debug_nth_element_u32": (_i, [_vp, _i, _i]),

@@ -2037,6 +2037,9 @@ struct orb_extractor {
     CellGeom* d_cells = nullptr;
     // per-stage HIP-event timing (orb_profile_*): stage k brackets its kernel(s) on the launch stream
     static constexpr int kStages = 5;
+    // phases run by the next launches: bit 0 = pyramid (stages 0-1), bit 1 = detection,
+    // selection and descriptors (stages 2-4, reading the pyramid bit 0 left in the workspace)
+    unsigned phaseMask = 3u;
     bool prof = false;
     unsigned profMask = 0;           // stages that record events (bit k = stage k)
     std::vector<hipEvent_t> evPool;  // 2 per stage per launch, recycled after each read
@@ -2422,6 +2425,7 @@ struct orb_extractor {
             int r = profile_collect();
             if (r) return r;
         }
+        if (phaseMask & 1u) {
         stage_begin(0, st);
         {
             const LevelGeom& lg = g.lv[0];
@@ -2444,6 +2448,11 @@ struct orb_extractor {
             hipLaunchKernelGGL(k_pyr_resize_tail, dim3(B), dim3(RT_THREADS), tailLds, st, d_pyr, d_rtab, g, resizeTail,
                                tailBufA, tailBufB);
         stage_end(1, st);
+        }
+        if (!(phaseMask & 2u)) {
+            HIP_TRY(hipGetLastError());
+            return ORB_OK;
+        }
         stage_begin(2, st);
         HIP_TRY(hipMemsetAsync(d_cellCount, 0, (size_t)g.nCells * B * 4, st));
         hipLaunchKernelGGL(k_level, dim3(nTiles, B), dim3(256), 0, st, d_pyr, d_blur, g, d_tiles, d_cells, d_cand,
@@ -2789,6 +2798,13 @@ static const char* kStageNames[] = {"k_pyr0", "k_pyr_resize", "k_level", "k_sele
 
 int orb_profile_enable(orb_extractor_t* h, int enable) {
     return orb_profile_enable_stages(h, enable ? (1u << orb_extractor::kStages) - 1u : 0u);
+}
+
+int orb_extract_set_phases(orb_extractor_t* h, unsigned phase_mask) {
+    if (!h) return set_err(ORB_EINVAL, "bad handle");
+    if (phase_mask == 0u || (phase_mask & ~3u)) return set_err(ORB_EINVAL, "phase_mask must be 1, 2 or 3");
+    h->phaseMask = phase_mask;
+    return ORB_OK;
 }
 
 int orb_profile_enable_stages(orb_extractor_t* h, unsigned stage_mask) {

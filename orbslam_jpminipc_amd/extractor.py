@@ -163,6 +163,11 @@ class ORBextractor:
         return d_kps, d_desc, d_counts
 
     # ---- measurement ----------------------------------------------------------------------
+    def set_phases(self, mask: int) -> None:
+        """Run only part of extract_batch_device on the next calls: 1 = pyramid, 2 = detection
+        through descriptors (reads the pyramid phase 1 left), 3 = both (default)."""
+        check(self._lib.orb_extract_set_phases(self._h, int(mask)))
+
     def profile_enable(self, enable: bool = True) -> None:
         """Record a HIP-event pair around every kernel stage of extract_batch_device."""
         check(self._lib.orb_profile_enable(self._h, int(enable)))

@@ -174,6 +174,36 @@ def test_batch_device_equals_single():
         assert outs[b][0].tobytes() == kps[b, : counts[b]].tobytes()
 
 
+def test_phase_split_equals_whole():
+    """orb_extract_set_phases: pyramid (1) then the rest (2), with another batch's pyramid and
+    extraction in between on a second extractor, is bit-identical to one mask-3 launch."""
+    import torch
+
+    B, W, H = 4, 640, 480
+    frames = orb.synth_stream(W, H, stream=3, first=0, count=B)
+    other = orb.synth_stream(W, H, stream=4, first=0, count=B)
+    ext = orb.ORBextractor(1000, 1.2, 8, orb.FAST_SCORE, 20, device=0, max_batch=B)
+    ext2 = orb.ORBextractor(1000, 1.2, 8, orb.FAST_SCORE, 20, device=0, max_batch=B)
+    d, d2 = torch.from_numpy(frames).cuda(), torch.from_numpy(other).cuda()
+    whole = [t.clone() for t in ext.extract_batch_device(d)]
+    ext.set_phases(1)
+    ext.extract_batch_device(d)
+    ext2.extract_batch_device(d2)
+    ext.set_phases(2)
+    split = ext.extract_batch_device(d)
+    ext.set_phases(3)
+    torch.cuda.synchronize()
+    n = whole[2].cpu().numpy()
+    assert (split[2].cpu().numpy() == n).all()
+    for b in range(B):
+        assert split[0][b, : n[b]].cpu().numpy().tobytes() == whole[0][b, : n[b]].cpu().numpy().tobytes()
+        assert split[1][b, : n[b]].cpu().numpy().tobytes() == whole[1][b, : n[b]].cpu().numpy().tobytes()
+    with pytest.raises(Exception):
+        ext.set_phases(0)
+    with pytest.raises(Exception):
+        ext.set_phases(4)
+
+
 @pytest.mark.parametrize("W,H,nf", [(640, 480, 1000), (640, 480, 2000), (1241, 376, 2000)])
 def test_search_for_initialization_parity(W, H, nf):
     ext = orb.ORBextractor(nf, 1.2, 8, orb.FAST_SCORE, 20, device=0)
