@@ -393,7 +393,9 @@ const char* orb_profile_stage_name(int i);
  * ORBextractor.cc:578-708, 749-778), which read the pyramid that bit 0 left in the extractor's
  * workspace.  A caller running phase 1 then phase 2 for the same batch, on one stream or
  * event-ordered, gets exactly the mask-3 result; the gap between them lets other work (the
- * previous batch's matching) overlap the pyramid.  Default 3.  No reference counterpart. */
+ * previous batch's matching) overlap the pyramid.  Default 3.  Applies to
+ * orb_extract_batch_device only; every other extraction entry point runs both phases.
+ * No reference counterpart. */
 int orb_extract_set_phases(orb_extractor_t* h, unsigned phase_mask);
 
 /* ---- test hooks (no device work unless stated) ------------------------------------- */

@@ -2037,8 +2037,9 @@ struct orb_extractor {
     CellGeom* d_cells = nullptr;
     // per-stage HIP-event timing (orb_profile_*): stage k brackets its kernel(s) on the launch stream
     static constexpr int kStages = 5;
-    // phases run by the next launches: bit 0 = pyramid (stages 0-1), bit 1 = detection,
-    // selection and descriptors (stages 2-4, reading the pyramid bit 0 left in the workspace)
+    // phases run by orb_extract_batch_device (the other entry points always run both):
+    // bit 0 = pyramid (stages 0-1), bit 1 = detection, selection and descriptors (stages 2-4,
+    // reading the pyramid bit 0 left in the workspace)
     unsigned phaseMask = 3u;
     bool prof = false;
     unsigned profMask = 0;           // stages that record events (bit k = stage k)
@@ -2420,12 +2421,12 @@ struct orb_extractor {
     }
 
     int launch(int B, const uint8_t* d_imgs, int stride, long long fpitch, orb_keypoint_t* kps, uint8_t* desc,
-               int* counts, hipStream_t st, int cn = 1, int rgb = 0) {
+               int* counts, hipStream_t st, int cn = 1, int rgb = 0, unsigned phases = 3u) {
         if (prof && evNext > 4096) {  // bound the pool between reads
             int r = profile_collect();
             if (r) return r;
         }
-        if (phaseMask & 1u) {
+        if (phases & 1u) {
         stage_begin(0, st);
         {
             const LevelGeom& lg = g.lv[0];
@@ -2449,7 +2450,7 @@ struct orb_extractor {
                                tailBufA, tailBufB);
         stage_end(1, st);
         }
-        if (!(phaseMask & 2u)) {
+        if (!(phases & 2u)) {
             HIP_TRY(hipGetLastError());
             return ORB_OK;
         }
@@ -2581,7 +2582,7 @@ int orb_extract_batch_device(orb_extractor_t* h, int B, const uint8_t* d_imgs, i
         if (r) return r;
     }
     h->lastStream = st;
-    return h->launch(B, d_imgs, stride, frame_pitch, d_kps, d_desc, d_counts, st);
+    return h->launch(B, d_imgs, stride, frame_pitch, d_kps, d_desc, d_counts, st, 1, 0, h->phaseMask);
 }
 
 int orb_extract_batch(orb_extractor_t* h, int B, const uint8_t* imgs, int w, int hgt, int stride, int64_t frame_pitch,

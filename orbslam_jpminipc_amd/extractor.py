@@ -164,8 +164,9 @@ class ORBextractor:
 
     # ---- measurement ----------------------------------------------------------------------
     def set_phases(self, mask: int) -> None:
-        """Run only part of extract_batch_device on the next calls: 1 = pyramid, 2 = detection
-        through descriptors (reads the pyramid phase 1 left), 3 = both (default)."""
+        """Run only part of extract_batch_device (not the other entry points) on the next
+        calls: 1 = pyramid, 2 = detection through descriptors (reads the pyramid phase 1 left),
+        3 = both (default)."""
         check(self._lib.orb_extract_set_phases(self._h, int(mask)))
 
     def profile_enable(self, enable: bool = True) -> None:

@@ -198,6 +198,12 @@ def test_phase_split_equals_whole():
     for b in range(B):
         assert split[0][b, : n[b]].cpu().numpy().tobytes() == whole[0][b, : n[b]].cpu().numpy().tobytes()
         assert split[1][b, : n[b]].cpu().numpy().tobytes() == whole[1][b, : n[b]].cpu().numpy().tobytes()
+    # the host-buffer entry point ignores the phase mask
+    ext.set_phases(1)
+    outs = ext.extract_batch(frames)
+    ext.set_phases(3)
+    for b in range(B):
+        assert outs[b][0].tobytes() == whole[0][b, : n[b]].cpu().numpy().tobytes()
     with pytest.raises(Exception):
         ext.set_phases(0)
     with pytest.raises(Exception):
