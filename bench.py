@@ -1,41 +1,74 @@
 #!/usr/bin/env python3
-"""bench.py — BASELINE.json's metric: frames/s of ORB extract + match on 640x480 frames.
+"""bench.py — BASELINE.json's metric: frames/s of ORB extract + match, with HBM GB/s vs peak.
 
-A step = one pass of the hot path over one batch of B synthetic 640x480 frames resident in
-HBM: ORBextractor(1000, 1.2, 8, FAST, 20) on all B frames (orb_extract_batch_device), then
-ORBmatcher(0.9, true).SearchForInitialization(F_t, F_t+1, window 100) on the B-1
-consecutive pairs (orb_search_for_initialization_batch_device), on one stream.  --overlap 1
-runs the steps as a two-stage stream pipeline instead (step t extracts batch t while batch t-1
-is matched on a second stream; the serial step is then reported beside it as "serial_step"):
-measured equal to the serial step on MI355X (1.80 vs 1.79 ms), so it is off by default.
-N GPUs run N independent
-replicas (frames shard one stream per GPU; no collectives on the data path); value is the
-whole-job frames/s = N * B * K / max-over-ranks(time of K steps).
+A step = one pass of the hot path over one batch of synthetic frames resident in HBM:
+ORBextractor(nfeatures, 1.2, 8, FAST, 20) on all B frames of the rank (orb_extract_batch_device),
+then ORBmatcher(0.9, true).SearchForInitialization(F_t, F_t+1, window 100) on every pair of
+consecutive frames of the same camera stream (orb_search_for_initialization_batch_device), both
+on one stream.  value = whole-job frames/s = (frames of all ranks per step) * K / max-over-ranks
+(time of K steps).
 
-Also reported (DESIGN.md §Measurement):
-  roofline      dominant kernel: algorithmic bytes per launch / mean launch duration, from
-                HIP events recorded around that stage on its launch stream inside the timed
-                region (an untimed survey pass brackets every stage to find it and to fill the
-                per-stage table; each event pair costs a ~10 us stream boundary).
-  pipeline      whole-path algorithmic bytes (SURVEY.md §8d B_ext + B_match) / wall time.
-  cpu_baseline  the CPU oracle (C++ restatement, oracle/) on the host cores, rank 0 only,
-                on a bounded sample of the same frames.
+Workloads (--workload; BASELINE.json configs):
+  c3  (default) configs[1]+[2]: 640x480, 1000 kp, B = 512 frames of camera stream `rank` per
+      GPU (weak scaling: every rank its own stream)
+  c4  configs[3]: KITTI-shaped 1241x376, 2000 kp, B = 512 frames of stream `rank` per GPU
+  c5  configs[4]: 8 independent 1280x720 camera streams, 2500 kp; stream s runs on rank
+      s mod N, --frames-per-stream frames of each per step (strong scaling:
+      the 8 streams are the whole job)
+
+Multi-GPU = replicas only (frames are independent, matching pairs frames of one
+stream; no data-path collective).  `python bench.py --gpus N` spawns N rank processes itself
+(RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 set before any GPU call, one per
+GPU); under torch.distributed.run the ranks come from the environment.  The only collectives
+are the barriers around the timed region, the max over ranks of its duration and a gather of
+the per-rank durations (rank_seconds).
+
+Also reported (DESIGN.md §6):
+  roofline      dominant kernel: SURVEY.md §8d algorithmic bytes of its stage per launch / mean
+                launch duration, from HIP events recorded around that stage on its launch stream
+                inside the timed region; traffic = PMC-measured HBM bytes per launch of the same
+                kernel (profiles/pmc_<workload>.json, rocprofv3 FETCH_SIZE / WRITE_SIZE passes)
+  pipeline      whole-path algorithmic bytes (§8d B_ext + B_match) / step time
+  latency_b1    the per-frame path the reference calls (Frame.cc:60, Tracking.cc:392-393): one
+                host frame through orb_extract, one frame pair through the host
+                SearchForInitialization, one device frame through orb_extract_batch_device; the
+                single-thread CPU oracle beside each (rank 0, N = 1)
+  cpu_baseline  the CPU oracle (C++ restatement, oracle/) on the host cores, rank 0, N = 1, on a
+                bounded sample of the same frames: extract-only and extract+match frames/s on all
+                threads, single-thread ms/frame, CPU model
+--overlap 1 / 2 are measured-slower stream-overlap experiments; the default (0)
+is the serial step.  --dry-run runs the launcher and rank plumbing on CPU (gloo, the oracle as
+the per-rank workload) for the multi-process tests.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 import numpy as np
-import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md §Chip-level parameters)
+METRIC = "frames/sec ORB extract+match, 640x480 8-level 1000 kp; HBM GB/s vs peak"
+
+WORKLOADS = {
+    "c3": dict(W=640, H=480, nf=1000, streams=0,
+               label="BASELINE.json configs[1]+[2]: batched 640x480 frames, ORBextractor(1000,1.2,8,FAST,20) + "
+                     "SearchForInitialization(t,t+1) nnratio 0.9 checkOri window 100"),
+    "c4": dict(W=1241, H=376, nf=2000, streams=0,
+               label="BASELINE.json configs[3]: KITTI-shaped 1241x376 frames, ORBextractor(2000,1.2,8,FAST,20) + "
+                     "SearchForInitialization(t,t+1) nnratio 0.9 checkOri window 100"),
+    "c5": dict(W=1280, H=720, nf=2500, streams=8,
+               label="BASELINE.json configs[4]: 8 independent 1280x720 streams (stream s on GPU s mod N), "
+                     "ORBextractor(2500,1.2,8,FAST,20) + SearchForInitialization(t,t+1) within each stream"),
+}
 
 
 def level_sizes(W, H, nlevels=8, scale=1.2):
@@ -50,34 +83,31 @@ def level_sizes(W, H, nlevels=8, scale=1.2):
     return out
 
 
-def stage_bytes(W, H, n_kp, n_cand, n_pairs_kp0, B):
-    """Algorithmic HBM bytes per launch of each stage for a batch of B frames.
-
-    n_kp: total keypoints of the batch; n_cand: total FAST survivors; n_pairs_kp0: sum over
-    pairs of (n1_0 + n2_0) level-0 keypoints.  Definitions in DESIGN.md §Roofline.
-    """
+def stage_bytes(W, H, n_kp, B):
+    """SURVEY.md §8d algorithmic bytes per launch of each extraction stage for B frames:
+    B_ext = sum_l w_l h_l (each level read once) + sum_{l>=1} w_l h_l (each derived level
+    written once) + 60 N_kp (keypoint + descriptor records written), split over the stages
+    that carry each term: the level-0 input read by k_pyr0, the derived levels written by the
+    resize stage (per launch: per level), every level read by k_level (detection), the records
+    written by k_orient_desc.  Nothing else counts (padding, intermediates, re-reads)."""
     lv = level_sizes(W, H)
-    pad = [(w + 32) * (h + 32) for w, h in lv]
     px = [w * h for w, h in lv]
     return {
-        "k_pyr0": B * (W * H + pad[0]),
-        "k_pyr_resize": B * sum(px[l - 1] + pad[l] for l in range(1, len(lv))) / (len(lv) - 1),  # per launch
-        # blur + FAST: read the level with its 3/4 px halo once, write the blurred ROI + border
-        "k_level": B * sum(2 * (w + 8) * (h + 6) for w, h in lv),
-        # read the level corner lists (>= survivors), write the cell candidates
-        "k_cell_nms": 8 * n_cand,
-        "k_select": 8 * n_cand + 4 * n_kp,
-        "k_orient_desc": n_kp * (4 + 31 * 31 + 512 + 60),
+        "k_pyr0": B * px[0],
+        "k_pyr_resize": B * sum(px[1:]) / (len(lv) - 1),
+        "k_level": B * sum(px),
+        "k_select": 0,
+        "k_orient_desc": 60 * n_kp,
     }
 
 
-def pmc_traffic(kernel, W, H, B, NF):
+def pmc_traffic(kernel, workload, W, H, B, NF):
     """HBM bytes per launch of `kernel` from the committed PMC summary of this workload
-    (profiles/pmc_latest.json, written by scripts/pmc_summary.py from rocprofv3 FETCH_SIZE /
-    WRITE_SIZE passes over bench.py) with the source tag and the kernel's SQ_INSTS_VALU (wave
-    instructions per launch), or Nones when the summary does not cover this run."""
+    (profiles/pmc_<workload>.json, scripts/pmc_summary.py over rocprofv3 FETCH_SIZE /
+    WRITE_SIZE passes of this bench), with the source tag and the kernel's SQ_INSTS_VALU, or
+    Nones when no summary covers this exact run shape."""
     try:
-        with open(os.path.join(ROOT, "profiles", "pmc_latest.json")) as f:
+        with open(os.path.join(ROOT, "profiles", f"pmc_{workload}.json")) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None, None, None
@@ -88,8 +118,19 @@ def pmc_traffic(kernel, W, H, B, NF):
     return (k["hbm_bytes"], d.get("source"), k.get("SQ_INSTS_VALU")) if k else (None, None, None)
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(frames, nfeatures, threads, W, H):
-    """Oracle (test infrastructure, oracle/liborb_oracle.so) on a bounded sample."""
+    """Oracle (test infrastructure, oracle/liborb_oracle.so) on a bounded sample: extract-only
+    and extract+match frames/s on `threads` threads, single-thread ms/frame."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import ctypes
 
@@ -99,33 +140,167 @@ def cpu_baseline(frames, nfeatures, threads, W, H):
     fr = np.ascontiguousarray(frames)
     k = ctypes.c_int64()
     m = ctypes.c_int64()
-    L.oracle_bench(nfeatures, 1.2, 8, 20, fr[:8].ctypes.data_as(ctypes.c_void_p), min(8, len(fr)), W, H, W, W * H,
-                   threads, 1, ctypes.byref(k), ctypes.byref(m))  # warm-up
-    dt = L.oracle_bench(nfeatures, 1.2, 8, 20, fr.ctypes.data_as(ctypes.c_void_p), len(fr), W, H, W, W * H, threads,
-                        1, ctypes.byref(k), ctypes.byref(m))
-    if dt <= 0:
-        raise RuntimeError("oracle_bench failed")
-    return len(fr) / dt, dt, int(k.value), int(m.value)
+    vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+
+    def run(sample, nthreads, match):
+        dt = L.oracle_bench(nfeatures, 1.2, 8, 20, vp(sample), len(sample), W, H, W, W * H, nthreads, match,
+                            ctypes.byref(k), ctypes.byref(m))
+        if dt <= 0:
+            raise RuntimeError("oracle_bench failed")
+        return dt
+
+    run(fr[:16], threads, 1)  # warm-up
+    t_ext = run(fr, threads, 0)
+    t_all = run(fr, threads, 1)
+    n1 = min(len(fr), 48)
+    t_one = run(fr[:n1], 1, 0)
+    t_one_m = run(fr[:n1], 1, 1)
+    return {
+        "extract_fps": len(fr) / t_ext,
+        "extract_match_fps": len(fr) / t_all,
+        "single_thread_ms_per_frame_extract": t_one / n1 * 1e3,
+        "single_thread_ms_per_frame_extract_match": t_one_m / n1 * 1e3,
+        "sample_frames": len(fr),
+        "single_thread_sample_frames": n1,
+        "wall_s": t_ext + t_all + t_one + t_one_m,
+    }
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=512, help="frames per step per GPU")
-    ap.add_argument("--width", type=int, default=640)
-    ap.add_argument("--height", type=int, default=480)
-    ap.add_argument("--nfeatures", type=int, default=1000)
-    ap.add_argument("--cpu-frames", type=int, default=3072,
-                    help="CPU-baseline sample size (0 = skip); ~20 s of CPU-thread time on 16 threads")
-    ap.add_argument("--overlap", type=int, default=0,
-                    help="1: extract(t) on one stream while matching batch t-1 on another; 2: only the "
-                         "pyramid of batch t overlaps the matching of batch t-1; 0: serial step")
-    ap.add_argument("--survey-steps", type=int, default=5, help="untimed steps with every stage bracketed")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = OMP_NUM_THREADS or os.cpu_count()")
-    args = ap.parse_args()
-    args.survey_steps = max(1, args.survey_steps)
+# ---------------------------------------------------------------------------------------------
+# launcher: N rank processes, spawned before anything touches a GPU
+# ---------------------------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_replicas(n):
+    """Start n copies of this script as ranks 0..n-1 (fresh processes, so the GPU is first
+    touched inside each rank) and relay rank 0's output; exit code = the first failing rank's."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out0 = procs[0].communicate()[0]
+    rcs = [procs[0].returncode] + [p.wait() for p in procs[1:]]
+    sys.stdout.write(out0.decode())
+    sys.stdout.flush()
+    return next((rc for rc in rcs if rc), 0)
+
+
+# ---------------------------------------------------------------------------------------------
+# the CPU dry run (launcher / rank plumbing tests)
+# ---------------------------------------------------------------------------------------------
+def run_dry(args):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_lib import Oracle
+
+    import orbslam_jpminipc_amd as orb
+    from orbslam_jpminipc_amd import replicas
+
+    info = replicas.init_from_env("gloo")
+    W, H, B = 160, 120, 2
+    frames = orb.synth_stream(W, H, stream=info.rank, first=0, count=B)
+    ora = Oracle(300, 1.2, 4, 1, 20)
+    for _ in range(args.warmup):
+        for f in frames:
+            ora.extract(f)
+    replicas.barrier(info)
+    t0 = time.perf_counter()
+    n = 0
+    for _ in range(args.steps):
+        for f in frames:
+            n += len(ora.extract(f)[0])
+    dt = time.perf_counter() - t0
+    replicas.barrier(info)
+    tmax = replicas.max_over_ranks(dt, info)
+    ranks = replicas.gather_over_ranks(dt, info)
+    if info.rank == 0:
+        print(json.dumps({"metric": METRIC, "value": replicas.whole_job_rate(B * args.steps, info.world, tmax),
+                          "unit": "frames/s", "n_gpus": info.world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": tmax / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+                          "vs_baseline": None, "dtype": "u8", "data": "synthetic (dry run: CPU oracle, 160x120)",
+                          "config": {"workload": "dry run (launcher plumbing)", "parallelism":
+                                     f"replicas x{info.world} (no collectives)"},
+                          "rank_seconds": ranks, "keypoints": n}))
+    replicas.shutdown(info)
+    return 0
+
+
+# ---------------------------------------------------------------------------------------------
+# one GPU rank
+# ---------------------------------------------------------------------------------------------
+def latency_b1(orb, W, H, NF, device, frames, reps=100):
+    """Per-call latency of the reference's per-frame path (rank 0, N = 1)."""
+    import torch
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_lib import Oracle, search_for_initialization
+
+    f0, f1 = frames[0].copy(), frames[1].copy()
+    ext = orb.ORBextractor(NF, 1.2, 8, orb.FAST_SCORE, 20, device=device, max_batch=1)
+    for _ in range(10):
+        ext(f0)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        k0, d0 = ext(f0)
+    t_ext = (time.perf_counter() - t0) / reps
+    k1, d1 = ext(f1)
+    F1 = orb.Frame(k0, d0, W, H)
+    F2 = orb.Frame(k1, d1, W, H)
+    prev0 = np.ascontiguousarray(np.stack([F1.mvKeys["x"], F1.mvKeys["y"]], 1).astype(np.float32))
+    M = orb.ORBmatcher(0.9, True)
+    m12 = []
+    for _ in range(10):
+        M.SearchForInitialization(F1, F2, prev0.copy(), m12, 100)
+    t_sfi = 0.0
+    for _ in range(reps):
+        p = prev0.copy()
+        t0 = time.perf_counter()
+        M.SearchForInitialization(F1, F2, p, m12, 100)
+        t_sfi += time.perf_counter() - t0
+    t_sfi /= reps
+    # device-resident frame: the kernel chain alone (launches + one stream sync)
+    d = torch.from_numpy(f0.reshape(1, H, W).copy()).cuda(device)
+    s = torch.cuda.Stream(device)
+    outs = ext.extract_batch_device(d, stream=s)
+    s.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ext.extract_batch_device(d, *outs, stream=s)
+        s.synchronize()
+    t_dev = (time.perf_counter() - t0) / reps
+    ora = Oracle(NF, 1.2, 8, 1, 20)
+    ora.extract(f0)
+    n_cpu = 20
+    t0 = time.perf_counter()
+    for _ in range(n_cpu):
+        ora.extract(f0)
+    c_ext = (time.perf_counter() - t0) / n_cpu
+    t0 = time.perf_counter()
+    for _ in range(n_cpu):
+        search_for_initialization(F1.mvKeys, F1.mDescriptors, F2.mvKeys, F2.mDescriptors, W, H, prev0.copy(), 0.9,
+                                  True, 100)
+    c_sfi = (time.perf_counter() - t0) / n_cpu
+    return {
+        "orb_extract_host_ms": t_ext * 1e3,
+        "orb_extract_device_b1_ms": t_dev * 1e3,
+        "search_for_initialization_host_ms": t_sfi * 1e3,
+        "cpu_oracle_single_thread_extract_ms": c_ext * 1e3,
+        "cpu_oracle_single_thread_sfi_ms": c_sfi * 1e3,
+        "note": f"{W}x{H}, {NF} kp, {reps} calls each through the Python binding (ctypes); host entries include "
+                "H2D/D2H and a stream synchronisation per call",
+    }
+
+
+def run_rank(args):
+    import torch
 
     import orbslam_jpminipc_amd as orb
     from orbslam_jpminipc_amd import replicas
@@ -133,9 +308,21 @@ def main():
     info = replicas.init_from_env("nccl")
     world, rank, local = info.world, info.rank, info.local_rank
     torch.cuda.set_device(local)
-
-    W, H, B, NF = args.width, args.height, args.batch, args.nfeatures
-    frames = orb.synth_stream(W, H, stream=rank, first=0, count=B)
+    wl = WORKLOADS[args.workload]
+    W = args.width or wl["W"]
+    H = args.height or wl["H"]
+    NF = args.nfeatures or wl["nf"]
+    custom = (W, H, NF) != (wl["W"], wl["H"], wl["nf"])
+    if wl["streams"]:
+        if world > wl["streams"]:
+            raise SystemExit(f"{args.workload}: {wl['streams']} streams cannot feed {world} ranks")
+        my_streams = replicas.streams_of_rank(wl["streams"], rank, world)
+        per = args.frames_per_stream
+    else:
+        my_streams = [rank]
+        per = args.batch
+    B = per * len(my_streams)
+    frames = np.concatenate([orb.synth_stream(W, H, stream=s, first=0, count=per) for s in my_streams])
     d_imgs = torch.from_numpy(frames).cuda()
     ext = orb.ORBextractor(NF, 1.2, 8, orb.FAST_SCORE, 20, device=local, max_batch=B)
     matcher = orb.ORBmatcher(0.9, True)
@@ -143,13 +330,15 @@ def main():
     d_kps = torch.empty((B, cap, 28), dtype=torch.uint8, device="cuda")
     d_desc = torch.empty((B, cap, 32), dtype=torch.uint8, device="cuda")
     d_cnt = torch.empty((B,), dtype=torch.int32, device="cuda")
-    f1 = torch.arange(0, B - 1, dtype=torch.int32, device="cuda")
+    # pairs (t, t+1) inside each stream's run of frames
+    f1 = torch.tensor([k * per + t for k in range(len(my_streams)) for t in range(per - 1)], dtype=torch.int32,
+                      device="cuda")
     f2 = f1 + 1
-    # serial mode: one stream carries the whole step, extraction then the matching that reads
-    # its output.  overlap mode (default): a two-stage stream pipeline over consecutive batches —
-    # step t extracts batch t on s_ext while s_match runs SearchForInitialization on batch t-1
-    # (double-buffered outputs, event-ordered); every step still does B extractions and B-1
-    # pair matches, so steps/s is the same work rate.
+    P = int(f1.numel())
+    # serial mode (default): one stream carries the whole step, extraction then the matching that
+    # reads its output.  --overlap 1 / 2 (measured slower): a two-stage stream
+    # pipeline over consecutive batches, step t extracting batch t (or only its pyramid) while
+    # s_match runs SearchForInitialization on batch t-1 (double-buffered, event-ordered).
     s_ext = torch.cuda.Stream()
     s_match = torch.cuda.Stream()
     torch.cuda.current_stream().synchronize()  # inputs uploaded on the default stream
@@ -179,8 +368,6 @@ def main():
         st["t"] += 1
         cur, prev = t % 2, (t - 1) % 2
         if st["overlap"] == 2:
-            # pyramid(t) || match(t-1); detection..descriptors of t after match(t-1), so the
-            # matcher's LDS-heavy work-groups never share the chip with k_level's
             with torch.cuda.stream(s_ext):
                 ext.set_phases(1)
                 ext.extract_batch_device(d_imgs, *bufs[cur], stream=s_ext)
@@ -255,6 +442,7 @@ def main():
     prof[dom] = live  # the dominant stage: measured inside the timed region
 
     tmax = replicas.max_over_ranks(elapsed, info)
+    rank_seconds = replicas.gather_over_ranks(elapsed, info)
 
     # workload statistics of the last step (identical every step: same frames)
     cnt = d_cnt.cpu().numpy().astype(np.int64)
@@ -262,26 +450,13 @@ def main():
     oct0 = np.array([int((orb.keypoints_from_bytes(kps_h[b], cnt[b])["octave"] == 0).sum()) for b in range(B)])
     n_kp = int(cnt.sum())
     nm_h = nm.cpu().numpy()
-    n_cand = int(n_kp * 3)  # refined below from the FAST survivors when available
-    try:
-        import ctypes
-
-        lib = orb.hip_lib()
-        tot = 0
-        buf = np.zeros(4096, np.int32)
-        for b in range(B):
-            for l in range(8):
-                n = lib.orb_debug_cell_counts(ext._h, b, l, buf.ctypes.data_as(ctypes.c_void_p), 4096)
-                tot += int(buf[:n].sum())
-        n_cand = tot
-    except Exception:
-        pass
-    pairs_kp0 = int(sum(oct0[p] + oct0[p + 1] for p in range(B - 1)))
-    sb = stage_bytes(W, H, n_kp, n_cand, pairs_kp0, B)
+    f1h, f2h = f1.cpu().numpy(), f2.cpu().numpy()
+    sb = stage_bytes(W, H, n_kp, B)
     lv = level_sizes(W, H)
     px = [w * h for w, h in lv]
     b_ext = B * (sum(px) + sum(px[1:])) + 60 * n_kp
-    b_match = 32 * pairs_kp0 + 20 * int(sum(cnt[:-1]))
+    # SURVEY §8d B_match = 32 (N1 + N2) + 20 N1 per pair
+    b_match = int(sum(32 * (cnt[a] + cnt[b]) + 20 * cnt[a] for a, b in zip(f1h, f2h)))
     sb["k_match_init"] = b_match
     stages = {}
     for name, (ms, launches) in prof.items():
@@ -306,14 +481,16 @@ def main():
         s["note"] = "per pyramid level (levels 1-7; the small levels share one k_pyr_resize_tail launch)"
     ds = stages[dom]
     per_step_s = tmax / args.steps
+    frames_job = per * wl["streams"] if wl["streams"] else B * world  # every rank's frames of one step
 
-    value = replicas.whole_job_rate(B * args.steps, world, tmax)
-    traffic, traffic_src, valu_insts = pmc_traffic(dom, W, H, B, NF)
+    value = frames_job * args.steps / tmax
+    traffic, traffic_src, valu_insts = pmc_traffic(dom, args.workload, W, H, B, NF)
     # VALU issue ceiling: each SIMD issues one wave64 VALU instruction per 2 cycles
     # (MI355X_MICROARCH.md), 4 SIMDs x 256 CUs at 2.4 GHz
     valu_peak = 256 * 4 / 2 * 2.4e9
+    label = wl["label"] if not custom else f"custom {W}x{H}, ORBextractor({NF},1.2,8,FAST,20) + SearchForInitialization"
     result = {
-        "metric": "frames/sec ORB extract+match, 640x480 8-level 1000 kp; HBM GB/s vs peak",
+        "metric": METRIC,
         "value": value,
         "unit": "frames/s",
         "n_gpus": world,
@@ -321,22 +498,24 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": per_step_s * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if wl["streams"] else "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (csrc/synth.c: rectangles+discs+noise, consecutive frames shifted)",
+        "data": "synthetic (csrc/synth.c: rectangles+discs+noise, consecutive frames of a stream shifted)",
         "config": {
-            "workload": f"{W}x{H} frames, ORBextractor({NF},1.2,8,FAST,20) + SearchForInitialization(t,t+1) "
-                        f"nnratio 0.9 checkOri window 100 (BASELINE.json configs[1]+[2])",
+            "workload": label,
+            "preset": args.workload,
+            "width": W, "height": H, "nfeatures": NF,
             "batch_per_gpu": B,
-            "pairs_per_gpu": B - 1,
+            "pairs_per_gpu": P,
+            "streams_of_rank0": my_streams,
             "parallelism": f"replicas x{world} (no collectives)",
             "streams": {0: "one stream, extract then match",
                         1: "extract(t) || SearchForInitialization(t-1), double-buffered",
                         2: "pyramid(t) || SearchForInitialization(t-1), then the rest of extract(t)"}
                        [args.overlap],
         },
-
+        "rank_seconds": rank_seconds,
         "roofline": {
             "kernel": dom,
             "bound": "hbm",
@@ -348,6 +527,7 @@ def main():
             "traffic_unit": "bytes per launch (rocprofv3 PMC)",
             "traffic_source": traffic_src,
             "algorithmic_bytes_per_launch": ds["bytes_per_launch"],
+            "algorithmic_bytes_basis": "SURVEY.md §8d, this stage's terms only (bench.stage_bytes)",
             "valu_insts_per_launch": valu_insts,
             "valu_issue_frac": (valu_insts / (ds["ms_per_launch"] * 1e-3) / valu_peak) if valu_insts else None,
         },
@@ -357,29 +537,69 @@ def main():
             "frac": (b_ext + b_match) / per_step_s / 1e9 / HBM_PEAK_GBS,
         },
         "stages": stages,
-        "workload_stats": {"keypoints_per_frame": n_kp / B, "fast_survivors_per_frame": n_cand / B,
+        "workload_stats": {"keypoints_per_frame": n_kp / B, "octave0_per_frame": float(oct0.mean()),
                            "matches_per_pair": float(nm_h.mean())},
     }
     if args.overlap:
-        result["serial_step"] = {"value": replicas.whole_job_rate(B * args.steps, world, serial_tmax),
+        result["serial_step"] = {"value": frames_job * args.steps / serial_tmax,
                                  "ms_per_step": serial_tmax / args.steps * 1e3}
+    if rank == 0 and world == 1 and args.latency:
+        result["latency_b1"] = latency_b1(orb, W, H, NF, local, frames[:2])
     if rank == 0 and world == 1 and args.cpu_frames > 0:
         threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or os.cpu_count())
         ncpu = args.cpu_frames
         cpu_frames = orb.synth_stream(W, H, stream=0, first=0, count=ncpu)
-        fps, dt, _, _ = cpu_baseline(cpu_frames, NF, threads, W, H)
+        cb = cpu_baseline(cpu_frames, NF, threads, W, H)
         result["cpu_baseline"] = {
-            "value": fps,
+            "value": cb["extract_match_fps"],
             "unit": "frames/s",
             "cores": threads,
             "kind": "port",
-            "sample": f"{ncpu} frames extract + {ncpu - 1} consecutive-pair SearchForInitialization, "
-                      f"{dt:.2f} s wall on {threads} threads (C++ restatement oracle, -O3)",
+            "sample": f"{ncpu} frames of stream 0, extract + {ncpu - 1} consecutive-pair SearchForInitialization "
+                      f"(C++ restatement oracle, -O3 -march=native, scalar: not OpenCV's SSE2 build)",
+            "extract_fps": cb["extract_fps"],
+            "extract_match_fps": cb["extract_match_fps"],
+            "single_thread_ms_per_frame_extract": cb["single_thread_ms_per_frame_extract"],
+            "single_thread_ms_per_frame_extract_match": cb["single_thread_ms_per_frame_extract_match"],
+            "single_thread_sample_frames": cb["single_thread_sample_frames"],
+            "cpu_model": cpu_model(),
+            "logical_cpus_visible": os.cpu_count(),
+            "wall_s": cb["wall_s"],
         }
     if rank == 0:
         print(json.dumps(result))
     replicas.shutdown(info)
+    return 0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1, help="ranks; without torch.distributed.run this script spawns "
+                                                        "them itself")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3")
+    ap.add_argument("--batch", type=int, default=512, help="frames per step per GPU (c3, c4)")
+    ap.add_argument("--frames-per-stream", type=int, default=128, help="frames of each stream per step (c5)")
+    ap.add_argument("--width", type=int, default=0, help="override the preset (0 = preset)")
+    ap.add_argument("--height", type=int, default=0)
+    ap.add_argument("--nfeatures", type=int, default=0)
+    ap.add_argument("--cpu-frames", type=int, default=1536,
+                    help="CPU-baseline sample size (0 = skip); ~10 s of oracle wall time on 16 threads")
+    ap.add_argument("--latency", type=int, default=1, help="1: measure latency_b1 (rank 0, N = 1)")
+    ap.add_argument("--overlap", type=int, default=0,
+                    help="0 (default): serial step; 1 / 2: stream-overlap experiments, measured slower")
+    ap.add_argument("--survey-steps", type=int, default=5, help="untimed steps with every stage bracketed")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = OMP_NUM_THREADS or os.cpu_count()")
+    ap.add_argument("--dry-run", action="store_true", help="CPU only: launcher + rank plumbing with the oracle")
+    args = ap.parse_args()
+    args.survey_steps = max(1, args.survey_steps)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return launch_replicas(args.gpus)
+    if args.dry_run:
+        return run_dry(args)
+    return run_rank(args)
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

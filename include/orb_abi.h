@@ -136,7 +136,10 @@ int orb_search_for_initialization(const orb_keypoint_t* kps1, const uint8_t* des
  * orb_extract_batch_device (d_kps / d_desc / d_counts with per-frame capacity `cap`).
  *   d_prev_xy: P x cap x 2 floats (in/out); NULL means "vbPrevMatched = F1 keypoints"
  *              (Tracking::FirstInitialization, reference Tracking.cc:366-368) and no update.
- *   d_matches12: P x cap int32; d_nmatches: P int32.  Asynchronous on `stream`. */
+ *   d_matches12: P x cap int32; d_nmatches: P int32.  Asynchronous on `stream`.
+ * cap <= 8192.  Frames with up to 1024 octave-0 keypoints are matched with all state in LDS;
+ * pairs over that (e.g. the reference init extractor, nFeatures*2, at 1280x720) are redone by a
+ * large-capacity kernel on the same stream (stream-ordered scratch), so every pair is exact. */
 int orb_search_for_initialization_batch_device(const orb_keypoint_t* d_kps, const uint8_t* d_desc,
                                                const int32_t* d_counts, int cap, int P, const int32_t* d_pair_f1,
                                                const int32_t* d_pair_f2, orb_frame_bounds_t bounds, float nnratio,
@@ -328,6 +331,34 @@ int orb_compute_distinctive_descriptors_device(int M, const int32_t* d_offsets, 
                                                const uint8_t* d_usable, int max_obs, int32_t* d_best_row,
                                                uint8_t* d_out_desc, void* stream);
 
+/* ---- keyframe feature records of the reference's map files (csrc/orb_persist.hip) ---- */
+/* SaveWorldToFile / LoadWroldFromFile (reference include/SaveLoadWorld.h:1254, 2463) store each
+ * keyframe's features as one record per stream, little-endian as written on x86-64:
+ *   keypoint stream (kfKeyPoints.bin, kfKeyPointsUn.bin; SaveLoadWorld.h:1406-1443, read back at
+ *   2098-2160):   0xEB 0x90 | uint64 nKeys | nKeys x 28-byte cv::KeyPoint (= orb_keypoint_t)
+ *   descriptor stream (kfDescriptors.bin; SaveLoadWorld.h:1446-1460, read back at 2166-2189):
+ *                 0xEB 0x90 | int32 nDes | nDes x 32 bytes
+ * Readers report a wrong header through *header_ok = 0 and go on, as the reference's loader
+ * prints "header error ..., shouldn't" and keeps reading; a record longer than `len` is
+ * ORB_ERANGE.  *consumed = bytes of the record (the next record starts there). */
+size_t orb_keypoint_record_bytes(size_t n);
+size_t orb_descriptor_record_bytes(int n);
+int orb_write_keypoint_record(const orb_keypoint_t* kps, size_t n, uint8_t* out, size_t cap, size_t* written);
+int orb_read_keypoint_record(const uint8_t* in, size_t len, orb_keypoint_t* kps, size_t cap, size_t* n,
+                             size_t* consumed, int* header_ok);
+int orb_write_descriptor_record(const uint8_t* desc, int n, uint8_t* out, size_t cap, size_t* written);
+int orb_read_descriptor_record(const uint8_t* in, size_t len, uint8_t* desc, int cap, int* n, size_t* consumed,
+                               int* header_ok);
+/* B frames of orb_extract_batch_device output (per-frame capacity cap) packed on the device into
+ * both streams, one record per frame in frame order (what SaveWorldToFile writes for B keyframes):
+ * frame b's keypoint record at d_keys_stream + d_key_offsets[b], its descriptor record at
+ * d_des_stream + d_des_offsets[b]; d_*_offsets[B] = the stream lengths (B + 1 int64 each).
+ * keys_cap >= B * orb_keypoint_record_bytes(cap), des_cap >= B * orb_descriptor_record_bytes(cap);
+ * buffers 2-byte aligned.  Asynchronous on `stream`. */
+int orb_pack_keyframe_records_device(const orb_keypoint_t* d_kps, const uint8_t* d_desc, const int32_t* d_counts,
+                                     int cap, int B, uint8_t* d_keys_stream, size_t keys_cap, uint8_t* d_des_stream,
+                                     size_t des_cap, int64_t* d_key_offsets, int64_t* d_des_offsets, void* stream);
+
 /* ---- DBoW2 vocabulary (GPU: csrc/orb_voc.hip) -------------------------------------- */
 /* The reference's ORBVocabulary = DBoW2::TemplatedVocabulary<FORB::TDescriptor, FORB>
  * (include/ORBVocabulary.h).  A handle holds the tree on `device`; host entry points are
@@ -388,9 +419,9 @@ int orb_profile_read(orb_extractor_t* h, double* stage_ms, int64_t* stage_launch
 const char* orb_profile_stage_name(int i);
 
 /* Split orb_extract_batch_device into its two phases (scheduling only; results unchanged):
- * bit 0 = the image pyramid (ORBextractor.cc:1086-1117 ComputePyramid), bit 1 = detection,
- * selection, orientation and descriptors (ComputeKeyPointsOctTree + the descriptor loop,
- * ORBextractor.cc:578-708, 749-778), which read the pyramid that bit 0 left in the extractor's
+ * bit 0 = the image pyramid (ComputePyramid, ORBextractor.cc:781-822), bit 1 = detection,
+ * selection, orientation and descriptors (ComputeKeyPoints + the descriptor loop,
+ * ORBextractor.cc:522-707, 749-778), which read the pyramid that bit 0 left in the extractor's
  * workspace.  A caller running phase 1 then phase 2 for the same batch, on one stream or
  * event-ordered, gets exactly the mask-3 result; the gap between them lets other work (the
  * previous batch's matching) overlap the pyramid.  Default 3.  Applies to

@@ -153,6 +153,16 @@ HIP_SIGNATURES = {
     "orb_pipeline_profile_read": (_i, [_vp, _vp, _vp, _i]),
     "orb_compute_distinctive_descriptors": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _i]),
     "orb_compute_distinctive_descriptors_device": (_i, [_i, _vp, _vp, _vp, _i, _vp, _vp, _vp]),
+    "orb_keypoint_record_bytes": (ctypes.c_size_t, [ctypes.c_size_t]),
+    "orb_descriptor_record_bytes": (ctypes.c_size_t, [_i]),
+    "orb_write_keypoint_record": (_i, [_vp, ctypes.c_size_t, _vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),
+    "orb_read_keypoint_record": (_i, [_vp, ctypes.c_size_t, _vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t),
+                                      ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(_i)]),
+    "orb_write_descriptor_record": (_i, [_vp, _i, _vp, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),
+    "orb_read_descriptor_record": (_i, [_vp, ctypes.c_size_t, _vp, _i, ctypes.POINTER(_i),
+                                        ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(_i)]),
+    "orb_pack_keyframe_records_device": (_i, [_vp, _vp, _vp, _i, _i, _vp, ctypes.c_size_t, _vp, ctypes.c_size_t, _vp,
+                                              _vp, _vp]),
     "orb_vocabulary_load_text": (_i, [ctypes.c_char_p, _i, ctypes.POINTER(_vp)]),
     "orb_vocabulary_create": (_i, [_i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _i, ctypes.POINTER(_vp)]),
     "orb_vocabulary_destroy": (_i, [_vp]),

@@ -1636,17 +1636,26 @@ struct MatchGeom {
 
 // One workgroup (4 waves) per frame pair.
 //   phase 0  F2's octave-0, in-grid keypoints — the only possible candidates of
-//            GetFeaturesInArea(x, y, window, 0, 0) (Frame.cc:200-265) — are staged in LDS,
+//            GetFeaturesInArea(x, y, window, 0, 0) (Frame.cc:200-265) — are staged,
 //            ranked by grid-traversal order (ix, iy, index: Frame.cc:233-258), so a slot
 //            number IS the reference's candidate order; F1's octave-0 queries are listed in
 //            index order.
 //   phase 1  (parallel) every query's window candidates are scored; each keeps its 8
-//            smallest keys (dist << 11 | slot) = the reference's (distance, first-in-order).
+//            smallest keys (dist << KB | slot) = the reference's (distance, first-in-order).
 //   phase 2  (one wave, sequential: vMatchedDistance / vnMatches21 feed later queries)
 //            best = first candidate with vMatchedDistance > dist, second = the next such;
 //            if a truncated top-8 holds < 2 such candidates the wave rescans the window.
 //   phase 3  rotation histogram, ComputeThreeMaxima, vnMatches12 / vbPrevMatched out.
+// Two instantiations of the same body:
+//   k_match_init      every per-slot array in LDS (<= 1024 octave-0 keypoints per frame);
+//                     a pair with more leaves nmOut[p] = -2 for the fallback
+//   k_match_init_big  the fallback (reference init extractor at 1280x720: nFeatures*2 = 5000,
+//                     Tracking.cc:126/217, ~1086 level-0 keypoints): only the greedy state
+//                     (vMatchedDistance / vnMatches21, vnMatches12, bins) stays in LDS, the
+//                     staged descriptors / coordinates / top-8 lists live in a per-workgroup
+//                     global scratch slot (L2-resident); up to 8192 keypoints per frame.
 #define MATCH_TOPK 8
+#define MATCH_BIG_NMAX 8192
 #ifndef KM_SKIP1  // timing experiments only (wrong output): skip the phase-1 scan / phase 2
 #define KM_SKIP1 0
 #endif
@@ -1662,42 +1671,91 @@ __device__ __forceinline__ void topk_insert(uint32_t (&t)[MATCH_TOPK], uint32_t 
     }
 }
 
-__global__ void __launch_bounds__(256) k_match_init(const orb_keypoint_t* __restrict__ kps,
-                                                    const uint8_t* __restrict__ desc, const int* __restrict__ counts,
-                                                    int cap, int nmax, const int* __restrict__ pf1,
-                                                    const int* __restrict__ pf2, MatchGeom mg, float nnratio,
-                                                    int checkOri, float r, float* __restrict__ prev,
-                                                    int* __restrict__ m12out, int* __restrict__ nmOut) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+struct MatchArgs {
+    const orb_keypoint_t* kps;
+    const uint8_t* desc;
+    const int* counts;
+    int cap, nmax;
+    const int* pf1;
+    const int* pf2;
+    MatchGeom mg;
+    float nnratio;
+    int checkOri;
+    float r;
+    float* prev;
+    int* m12out;
+    int* nmOut;
+    int P;
+};
+
+// Byte size of one k_match_init_big global scratch slot (nmax slots / queries).
+__host__ __device__ inline size_t match_big_slot_bytes(int cap, int nmax) {
+    // d2 32 + x2,y2,a2,cell 16 per F2 slot; q2i,qx,qy,lcnt 16 per query; top-8 lists
+    // (also phase 0's key scratch: max(cap, 8 nmax) u32)
+    const size_t keys = (size_t)(cap > MATCH_TOPK * nmax ? cap : MATCH_TOPK * nmax);
+    return ((size_t)nmax * 64 + keys * 4 + 255) & ~(size_t)255;
+}
+
+template <bool BIG>
+__device__ __forceinline__ void match_pair(const MatchArgs& A, int p, uint8_t* __restrict__ smem,
+                                           uint8_t* __restrict__ gs) {
+    constexpr int KB = BIG ? 13 : 11;  // slot bits of a (distance, slot) key
+    constexpr uint32_t SLOT = (1u << KB) - 1u;
     __shared__ int s_n2c, s_n1c;
     __shared__ int s_hist[32];
     __shared__ int s_ind[3];
     __shared__ int s_col[65];  // first slot of grid column cx (slots are in (cx, cy, index) order)
-    const int p = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int f1 = pf1[p], f2 = pf2[p];
-    const int n1 = counts[f1], n2 = counts[f2];
-    const orb_keypoint_t* K1 = kps + (long long)f1 * cap;
-    const orb_keypoint_t* K2 = kps + (long long)f2 * cap;
-    const uint32_t* D1 = (const uint32_t*)(desc + (long long)f1 * cap * 32);
-    const uint32_t* D2 = (const uint32_t*)(desc + (long long)f2 * cap * 32);
-    uint32_t* s_d2 = (uint32_t*)smem;              // nmax x 8
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int cap = A.cap, nmax = A.nmax;
+    const MatchGeom mg = A.mg;
+    const float r = A.r, nnratio = A.nnratio;
+    float* __restrict__ prev = A.prev;
+    const int f1 = A.pf1[p], f2 = A.pf2[p];
+    const int n1 = A.counts[f1], n2 = A.counts[f2];
+    const orb_keypoint_t* K1 = A.kps + (long long)f1 * cap;
+    const orb_keypoint_t* K2 = A.kps + (long long)f2 * cap;
+    const uint32_t* D1 = (const uint32_t*)(A.desc + (long long)f1 * cap * 32);
+    const uint32_t* D2 = (const uint32_t*)(A.desc + (long long)f2 * cap * 32);
     // per F2 slot: x = vMatchedDistance (low 16 bits, 0xFFFF = INT_MAX) | (vnMatches21 + 1) << 16,
     // y = the F2 keypoint index — one LDS read gives the greedy pass all it needs of a slot
-    uint2* s_st = (uint2*)(s_d2 + (size_t)nmax * 8);
-    float* s_x2 = (float*)(s_st + nmax);
-    float* s_y2 = s_x2 + nmax;
-    int* s_cell = (int*)(s_y2 + nmax);              // posX * 48 + posY
-    int* s_q2i = s_cell + nmax;                     // query -> i1
-    float* s_qx = (float*)(s_q2i + nmax);
-    float* s_qy = s_qx + nmax;
-    float* s_a2 = s_qy + nmax;                      // F2 slot angle
-    uint32_t* s_list = (uint32_t*)(s_a2 + nmax);    // nmax x TOPK
-    int* s_lcnt = (int*)(s_list + (size_t)nmax * MATCH_TOPK);
-    int* s_m12 = s_lcnt + nmax;                     // vnMatches12 (cap)
-    short* s_bslot = (short*)(s_m12 + cap);         // F2 slot of each accepted i1, then its rotation bin (cap)
-    uint32_t* s_key = s_list;                       // phase-0 scratch (cap <= 8 * nmax)
+    uint32_t* s_d2;
+    uint2* s_st;
+    float *s_x2, *s_y2, *s_qx, *s_qy, *s_a2;
+    int *s_cell, *s_q2i, *s_lcnt, *s_m12;
+    uint32_t* s_list;
+    short* s_bslot;
+    if constexpr (!BIG) {
+        s_d2 = (uint32_t*)smem;  // nmax x 8
+        s_st = (uint2*)(s_d2 + (size_t)nmax * 8);
+        s_x2 = (float*)(s_st + nmax);
+        s_y2 = s_x2 + nmax;
+        s_cell = (int*)(s_y2 + nmax);  // posX * 48 + posY
+        s_q2i = s_cell + nmax;         // query -> i1
+        s_qx = (float*)(s_q2i + nmax);
+        s_qy = s_qx + nmax;
+        s_a2 = s_qy + nmax;                       // F2 slot angle
+        s_list = (uint32_t*)(s_a2 + nmax);        // nmax x TOPK
+        s_lcnt = (int*)(s_list + (size_t)nmax * MATCH_TOPK);
+        s_m12 = s_lcnt + nmax;                    // vnMatches12 (cap)
+        s_bslot = (short*)(s_m12 + cap);          // F2 slot of each accepted i1, then its rotation bin (cap)
+    } else {
+        s_st = (uint2*)smem;                      // LDS: greedy state
+        s_m12 = (int*)(s_st + nmax);
+        s_bslot = (short*)(s_m12 + cap);
+        s_d2 = (uint32_t*)gs;                     // global scratch slot
+        s_x2 = (float*)(s_d2 + (size_t)nmax * 8);
+        s_y2 = s_x2 + nmax;
+        s_cell = (int*)(s_y2 + nmax);
+        s_a2 = (float*)(s_cell + nmax);
+        s_q2i = (int*)(s_a2 + nmax);
+        s_qx = (float*)(s_q2i + nmax);
+        s_qy = s_qx + nmax;
+        s_lcnt = (int*)(s_qy + nmax);
+        s_list = (uint32_t*)(s_lcnt + nmax);
+    }
+    uint32_t* s_key = s_list;  // phase-0 scratch (cap entries)
     const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    // ---- phase 0: keys in parallel, then ordered compaction from LDS ----
+    // ---- phase 0: keys in parallel, then ordered compaction ----
     // s_key[i2] = traversal key of F2 keypoint i2 or ~0 (not octave 0 / outside the grid);
     // s_m12[i1] = 1 if F1 keypoint i1 is a query (octave 0), as scratch.
     for (int i = tid; i < n2; i += 256) {
@@ -1708,6 +1766,7 @@ __global__ void __launch_bounds__(256) k_match_init(const orb_keypoint_t* __rest
         s_key[i] = ok ? (((uint32_t)(px * 48 + py) << 16) | (uint32_t)i) : 0xFFFFFFFFu;
     }
     for (int i = tid; i < n1; i += 256) s_m12[i] = K1[i].octave == 0;  // level1 > 0 -> continue (ORBmatcher.cc:615)
+    if constexpr (BIG) __threadfence_block();
     __syncthreads();
     if (wave == 0) {  // in-place, in-order compaction (one wave: reads precede writes)
         int base = 0;
@@ -1730,10 +1789,11 @@ __global__ void __launch_bounds__(256) k_match_init(const orb_keypoint_t* __rest
         }
         if (lane == 0) s_n1c = base;
     }
+    if constexpr (BIG) __threadfence_block();
     __syncthreads();
     const int n2c = s_n2c, n1c = s_n1c;
-    if (n2c > nmax || n1c > nmax) {  // capacity exceeded: report, never truncate silently
-        if (tid == 0) nmOut[p] = -1;
+    if (n2c > nmax || n1c > nmax) {  // capacity exceeded: fall back / report, never truncate silently
+        if (tid == 0) A.nmOut[p] = BIG ? -1 : -2;
         return;
     }
     // rank F2 candidates by traversal key -> slot
@@ -1757,6 +1817,7 @@ __global__ void __launch_bounds__(256) k_match_init(const orb_keypoint_t* __rest
         s_qx[q] = prev ? prev[((long long)p * cap + i1) * 2] : kp.x;
         s_qy[q] = prev ? prev[((long long)p * cap + i1) * 2 + 1] : kp.y;
     }
+    if constexpr (BIG) __threadfence_block();
     __syncthreads();
     for (int i = tid; i < n1; i += 256) {
         s_m12[i] = -1;
@@ -1804,7 +1865,7 @@ __global__ void __launch_bounds__(256) k_match_init(const orb_keypoint_t* __rest
             if (cx < minCX || cx > maxCX || cy < minCY || cy > maxCY) continue;
             if (fabsf(s_x2[j] - qx) > r || fabsf(s_y2[j] - qy) > r) continue;
             const int dist = hamming256(d1, s_d2 + j * 8);
-            topk_insert(top, ((uint32_t)dist << 11) | (uint32_t)j);
+            topk_insert(top, ((uint32_t)dist << KB) | (uint32_t)j);
             ++cnt;
         }
         if (act) {
@@ -1813,6 +1874,7 @@ __global__ void __launch_bounds__(256) k_match_init(const orb_keypoint_t* __rest
             s_lcnt[q] = cnt;
         }
     }
+    if constexpr (BIG) __threadfence_block();
     __syncthreads();
     // ---- phase 2: the sequential greedy pass (ORBmatcher.cc:611-680) on one wave ----
     // Per query the critical path is one LDS read of its top-8 slots' state and scalar lane
@@ -1831,8 +1893,8 @@ __global__ void __launch_bounds__(256) k_match_init(const orb_keypoint_t* __rest
             }
             if (cnt == 0) continue;  // vIndices2.empty()
             const int k = min(cnt, MATCH_TOPK);
-            const uint2 st = lane < k ? s_st[e & 0x7FF] : make_uint2(0u, 0u);
-            const bool valid = lane < k && (int)(st.x & 0xFFFFu) > (int)(e >> 11);
+            const uint2 st = lane < k ? s_st[e & SLOT] : make_uint2(0u, 0u);
+            const bool valid = lane < k && (int)(st.x & 0xFFFFu) > (int)(e >> KB);
             const uint64_t m = __ballot(valid);
             uint32_t best, bst, bidx;
             int second;
@@ -1843,7 +1905,7 @@ __global__ void __launch_bounds__(256) k_match_init(const orb_keypoint_t* __rest
                 bst = (uint32_t)__builtin_amdgcn_readlane((int)st.x, e1);
                 bidx = (uint32_t)__builtin_amdgcn_readlane((int)st.y, e1);
                 const uint64_t m2 = m & (m - 1);
-                second = m2 ? (int)((uint32_t)__builtin_amdgcn_readlane((int)e, __ffsll((unsigned long long)m2) - 1) >> 11)
+                second = m2 ? (int)((uint32_t)__builtin_amdgcn_readlane((int)e, __ffsll((unsigned long long)m2) - 1) >> KB)
                             : 0x7fffffff;
             } else {
                 // exact rescan of the whole window
@@ -1865,9 +1927,9 @@ __global__ void __launch_bounds__(256) k_match_init(const orb_keypoint_t* __rest
                     if (fabsf(s_x2[j] - qx) > r || fabsf(s_y2[j] - qy) > r) continue;
                     const int dist = hamming256(d1, s_d2 + j * 8);
                     if ((int)(s_st[j].x & 0xFFFFu) <= dist) continue;
-                    const uint32_t key = ((uint32_t)dist << 11) | (uint32_t)j;
+                    const uint32_t key = ((uint32_t)dist << KB) | (uint32_t)j;
                     if (key < lb) {
-                        if (lb != 0xFFFFFFFFu) ls = (int)(lb >> 11);
+                        if (lb != 0xFFFFFFFFu) ls = (int)(lb >> KB);
                         lb = key;
                     } else if (dist < ls) {
                         ls = dist;
@@ -1877,17 +1939,17 @@ __global__ void __launch_bounds__(256) k_match_init(const orb_keypoint_t* __rest
 #pragma unroll
                 for (int o = 32; o >= 1; o >>= 1) gb = min(gb, (uint32_t)__shfl_xor((int)gb, o, 64));
                 if (gb == 0xFFFFFFFFu) continue;
-                int contrib = (lb == gb) ? ls : (lb == 0xFFFFFFFFu ? 0x7fffffff : (int)(lb >> 11));
+                int contrib = (lb == gb) ? ls : (lb == 0xFFFFFFFFu ? 0x7fffffff : (int)(lb >> KB));
 #pragma unroll
                 for (int o = 32; o >= 1; o >>= 1) contrib = min(contrib, __shfl_xor(contrib, o, 64));
                 best = gb;
                 second = contrib;
-                const uint2 sb = s_st[gb & 0x7FF];
+                const uint2 sb = s_st[gb & SLOT];
                 bst = sb.x;
                 bidx = sb.y;
             }
-            const int bestDist = (int)(best >> 11);
-            const int bestSlot = (int)(best & 0x7FF);
+            const int bestDist = (int)(best >> KB);
+            const int bestSlot = (int)(best & SLOT);
             if (bestDist <= 50 && (float)bestDist < (float)second * nnratio) {
                 // one wave: its LDS accesses complete in issue order, so lane 0's writes are
                 // seen by the next query's reads
@@ -1903,7 +1965,7 @@ __global__ void __launch_bounds__(256) k_match_init(const orb_keypoint_t* __rest
     }
     __syncthreads();
     // ---- phase 3 ----
-    if (checkOri) {
+    if (A.checkOri) {
         if (tid < 32) s_hist[tid] = 0;
         __syncthreads();
         // rotation bin of every accepted i1, the stolen ones included (ORBmatcher.cc:664-676)
@@ -1960,7 +2022,7 @@ __global__ void __launch_bounds__(256) k_match_init(const orb_keypoint_t* __rest
     int nm = 0;
     for (int i = tid; i < n1; i += 256) {
         const int m = s_m12[i];
-        m12out[(long long)p * cap + i] = m;
+        A.m12out[(long long)p * cap + i] = m;
         if (m >= 0) {
             nm++;
             if (prev) {
@@ -1973,7 +2035,25 @@ __global__ void __launch_bounds__(256) k_match_init(const orb_keypoint_t* __rest
     for (int o = 32; o >= 1; o >>= 1) nm += __shfl_xor(nm, o, 64);
     if (lane == 0) s_hist[wave] = nm;
     __syncthreads();
-    if (tid == 0) nmOut[p] = s_hist[0] + s_hist[1] + s_hist[2] + s_hist[3];
+    if (tid == 0) A.nmOut[p] = s_hist[0] + s_hist[1] + s_hist[2] + s_hist[3];
+    __syncthreads();  // s_hist / s_n*c are reused by the next pair of a big workgroup
+}
+
+__global__ void __launch_bounds__(256) k_match_init(MatchArgs A) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    match_pair<false>(A, blockIdx.x, smem, nullptr);
+}
+
+// The fallback over the pairs k_match_init left at -2: workgroup g owns global scratch slot g
+// and walks pairs g, g + gridDim.x, ... (grid <= P; a pair that fits exits at once).
+__global__ void __launch_bounds__(256) k_match_init_big(MatchArgs A, uint8_t* __restrict__ scratch) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t* gs = scratch + (size_t)blockIdx.x * match_big_slot_bytes(A.cap, A.nmax);
+    for (int p = blockIdx.x; p < A.P; p += gridDim.x) {
+        if (A.nmOut[p] != -2) continue;  // block-uniform
+        __syncthreads();
+        match_pair<true>(A, p, smem, gs);
+    }
 }
 
 // ======================================================================================
@@ -2009,7 +2089,10 @@ struct orb_extractor {
     int umax[16] = {};
     int kpCap = 0;
     hipStream_t stream = nullptr;      // the handle's own stream (host-buffer entry points)
-    hipStream_t lastStream = nullptr;  // stream of the last orb_extract_batch_device
+    hipStream_t lastStream = nullptr;  // stream of the last launch on this handle's workspace
+    bool lastValid = false;            // lastStream names a stream that ran a launch
+    hipEvent_t evOrder = nullptr;      // orders a launch after the previous one on another stream
+    int pyrBatch = 0;                  // frames whose pyramid phase 1 left in the workspace
     // geometry of the current frame size
     int W = 0, H = 0;
     Geom g{};
@@ -2050,6 +2133,8 @@ struct orb_extractor {
     int evNext = 0;
     // staging for host-buffer entry points
     uint8_t* d_img = nullptr;
+    uint8_t* d_imgColor = nullptr;  // orb_extract_color's interleaved frame
+    size_t imgColorCap = 0;
     orb_keypoint_t* d_kps = nullptr;
     uint8_t* d_desc = nullptr;
     int* d_counts = nullptr;
@@ -2075,6 +2160,7 @@ struct orb_extractor {
         hipFree(d_rtab);
         hipFree(d_cells);
         hipFree(d_img);
+        hipFree(d_imgColor);
         hipFree(d_kps);
         hipFree(d_desc);
         hipFree(d_counts);
@@ -2092,10 +2178,13 @@ struct orb_extractor {
         d_rtab = nullptr;
         d_cells = nullptr;
         d_img = nullptr;
+        d_imgColor = nullptr;
+        imgColorCap = 0;
         d_kps = nullptr;
         d_desc = nullptr;
         d_counts = nullptr;
         W = H = 0;
+        pyrBatch = 0;
     }
 
     // ORBextractor ctor arithmetic (ORBextractor.cc:462-510)
@@ -2395,20 +2484,27 @@ struct orb_extractor {
         }
         return evPool[evNext++];
     }
+    // stage_begin pushes one entry per bracketed stage; an entry whose events could not be
+    // created is a sentinel (index -1) that stage_end and profile_collect skip
     void stage_begin(int stage, hipStream_t st) {
         if (!prof || !((profMask >> stage) & 1u)) return;
         int i = evNext;
         hipEvent_t a = next_event(), b = next_event();
-        if (!a || !b) return;
-        hipEventRecord(a, st);
+        if (!a || !b || hipEventRecord(a, st) != hipSuccess) {
+            evPending.push_back({stage, -1});
+            return;
+        }
         evPending.push_back({stage, i});
     }
     void stage_end(int stage, hipStream_t st) {
         if (!prof || !((profMask >> stage) & 1u) || evPending.empty()) return;
-        hipEventRecord(evPool[evPending.back().second + 1], st);
+        const auto& pe = evPending.back();
+        if (pe.first != stage || pe.second < 0) return;
+        hipEventRecord(evPool[pe.second + 1], st);
     }
     int profile_collect() {
         for (auto& pe : evPending) {
+            if (pe.second < 0) continue;
             HIP_TRY(hipEventSynchronize(evPool[pe.second + 1]));
             float ms = 0.f;
             HIP_TRY(hipEventElapsedTime(&ms, evPool[pe.second], evPool[pe.second + 1]));
@@ -2420,8 +2516,30 @@ struct orb_extractor {
         return ORB_OK;
     }
 
+    // Every launch on this handle's workspace is ordered after the previous one, whatever
+    // stream either ran on: an event recorded on the previous stream is waited on by `st`
+    // (device-side; the host never blocks).
+    int order_after_last(hipStream_t st) {
+        if (lastValid && lastStream != st) {
+            HIP_TRY(hipEventRecord(evOrder, lastStream));
+            HIP_TRY(hipStreamWaitEvent(st, evOrder, 0));
+        }
+        lastStream = st;
+        lastValid = true;
+        return ORB_OK;
+    }
+    // The workspace is about to be re-allocated: drain every stream that may still use it.
+    int drain() {
+        HIP_TRY(hipStreamSynchronize(stream));
+        if (lastValid) HIP_TRY(hipStreamSynchronize(lastStream));
+        return ORB_OK;
+    }
+
     int launch(int B, const uint8_t* d_imgs, int stride, long long fpitch, orb_keypoint_t* kps, uint8_t* desc,
                int* counts, hipStream_t st, int cn = 1, int rgb = 0, unsigned phases = 3u) {
+        if (!(phases & 1u) && B > pyrBatch)
+            return set_err(ORB_EINVAL, "phase 2 without a phase-1 pyramid of this geometry for these frames");
+        if (int r = order_after_last(st)) return r;
         if (prof && evNext > 4096) {  // bound the pool between reads
             int r = profile_collect();
             if (r) return r;
@@ -2449,6 +2567,7 @@ struct orb_extractor {
             hipLaunchKernelGGL(k_pyr_resize_tail, dim3(B), dim3(RT_THREADS), tailLds, st, d_pyr, d_rtab, g, resizeTail,
                                tailBufA, tailBufB);
         stage_end(1, st);
+        pyrBatch = B;
         }
         if (!(phases & 2u)) {
             HIP_TRY(hipGetLastError());
@@ -2531,7 +2650,9 @@ int orb_extractor_create(int nfeatures, float scale_factor, int nlevels, int sco
     h->maxBatch = max_batch;
     h->init_params();
     hipError_t e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->evOrder, hipEventDisableTiming);
     if (e != hipSuccess) {
+        if (h->stream) (void)hipStreamDestroy(h->stream);
         delete h;
         return set_err(ORB_EDEVICE, std::string("hipStreamCreate: ") + hipGetErrorString(e));
     }
@@ -2542,9 +2663,10 @@ int orb_extractor_create(int nfeatures, float scale_factor, int nlevels, int sco
 int orb_extractor_destroy(orb_extractor_t* h) {
     if (!h) return ORB_OK;
     hipSetDevice(h->device);
-    hipStreamSynchronize(h->stream);
+    (void)h->drain();
     h->free_ws();
     h->free_events();
+    hipEventDestroy(h->evOrder);
     hipStreamDestroy(h->stream);
     delete h;
     return ORB_OK;
@@ -2576,12 +2698,10 @@ int orb_extract_batch_device(orb_extractor_t* h, int B, const uint8_t* d_imgs, i
     hipStream_t st = (hipStream_t)stream;  // NULL = the null stream, as everywhere in HIP
     if (w != h->W || hgt != h->H) {
         // the workspace is re-allocated: drain every stream that may still be using it
-        HIP_TRY(hipStreamSynchronize(h->stream));
-        HIP_TRY(hipStreamSynchronize(h->lastStream));
+        if (int r = h->drain()) return r;
         int r = h->build_geometry(w, hgt);
         if (r) return r;
     }
-    h->lastStream = st;
     return h->launch(B, d_imgs, stride, frame_pitch, d_kps, d_desc, d_counts, st, 1, 0, h->phaseMask);
 }
 
@@ -2593,10 +2713,12 @@ int orb_extract_batch(orb_extractor_t* h, int B, const uint8_t* imgs, int w, int
         return set_err(ORB_EINVAL, "bad image geometry");
     HIP_TRY(hipSetDevice(h->device));
     if (w != h->W || hgt != h->H) {
-        HIP_TRY(hipStreamSynchronize(h->stream));
+        if (int r = h->drain()) return r;
         int st = h->build_geometry(w, hgt);
         if (st) return st;
     }
+    // the copies below overwrite the staging a launch on another stream may still read
+    if (int r = h->order_after_last(h->stream)) return r;
     int st = h->ensure_staging();
     if (st) return st;
     HIP_TRY(hipMemcpy2DAsync(h->d_img, w, imgs, stride, w, (size_t)hgt, hipMemcpyHostToDevice, h->stream));
@@ -2644,12 +2766,10 @@ int orb_extract_batch_device_color(orb_extractor_t* h, int B, const uint8_t* d_i
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;
     if (w != h->W || hgt != h->H) {
-        HIP_TRY(hipStreamSynchronize(h->stream));
-        HIP_TRY(hipStreamSynchronize(h->lastStream));
+        if (int r = h->drain()) return r;
         int r = h->build_geometry(w, hgt);
         if (r) return r;
     }
-    h->lastStream = st;
     return h->launch(B, d_imgs, stride, frame_pitch, d_kps, d_desc, d_counts, st, channels, rgb);
 }
 
@@ -2665,29 +2785,36 @@ int orb_extract_color(orb_extractor_t* h, const uint8_t* img, int w, int hgt, in
     if (stride < w * channels) return set_err(ORB_EINVAL, "bad image geometry");
     HIP_TRY(hipSetDevice(h->device));
     if (w != h->W || hgt != h->H) {
-        HIP_TRY(hipStreamSynchronize(h->stream));
-        HIP_TRY(hipStreamSynchronize(h->lastStream));
+        if (int r = h->drain()) return r;
         int r = h->build_geometry(w, hgt);
         if (r) return r;
     }
+    if (int r = h->order_after_last(h->stream)) return r;
     int st = h->ensure_staging();
     if (st) return st;
     const size_t row = (size_t)w * channels;
-    uint8_t* dimg = nullptr;
-    HIP_TRY(hipMalloc(&dimg, row * hgt));
-    hipError_t e = hipMemcpy2DAsync(dimg, row, img, stride, row, (size_t)hgt, hipMemcpyHostToDevice, h->stream);
+    if (row * hgt > h->imgColorCap) {  // handle-owned, grow-only (the stream is ordered after every user)
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        (void)hipFree(h->d_imgColor);
+        h->d_imgColor = nullptr;
+        h->imgColorCap = 0;
+        HIP_TRY(hipMalloc(&h->d_imgColor, row * hgt));
+        h->imgColorCap = row * hgt;
+    }
+    HIP_TRY(hipMemcpy2DAsync(h->d_imgColor, row, img, stride, row, (size_t)hgt, hipMemcpyHostToDevice, h->stream));
     int32_t n = 0;
-    if (e == hipSuccess)
-        st = h->launch(1, dimg, (int)row, (long long)(row * hgt), h->d_kps, h->d_desc, h->d_counts, h->stream, channels,
-                       rgb);
-    if (e == hipSuccess && !st) e = hipMemcpyAsync(&n, h->d_counts, 4, hipMemcpyDeviceToHost, h->stream);
-    if (e == hipSuccess && !st) e = hipStreamSynchronize(h->stream);
-    (void)hipFree(dimg);
-    if (st) return st;
-    if (e != hipSuccess) return set_err(ORB_EDEVICE, std::string("colour extraction: ") + hipGetErrorString(e));
+    st = h->launch(1, h->d_imgColor, (int)row, (long long)(row * hgt), h->d_kps, h->d_desc, h->d_counts, h->stream,
+                   channels, rgb);
+    if (st) {
+        (void)hipStreamSynchronize(h->stream);
+        return st;
+    }
+    HIP_TRY(hipMemcpyAsync(&n, h->d_counts, 4, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
     if (n > kps_cap) return set_err(ORB_ERANGE, "kps_cap smaller than the number of keypoints");
-    HIP_TRY(hipMemcpy(kps_out, h->d_kps, (size_t)n * sizeof(orb_keypoint_t), hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(desc_out, h->d_desc, (size_t)n * 32, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpyAsync(kps_out, h->d_kps, (size_t)n * sizeof(orb_keypoint_t), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipMemcpyAsync(desc_out, h->d_desc, (size_t)n * 32, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
     *n_out = n;
     return ORB_OK;
 }
@@ -2708,6 +2835,7 @@ static size_t match_lds_bytes(int cap, int nmax) {
     // + cap x (m12 4 + slot/bin 2)
     return (size_t)nmax * (56 + 48) + (size_t)cap * 6 + 16;
 }
+static size_t match_big_lds_bytes(int cap, int nmax) { return (size_t)nmax * 8 + (size_t)cap * 6 + 16; }
 
 int orb_search_for_initialization_batch_device(const orb_keypoint_t* d_kps, const uint8_t* d_desc,
                                                const int32_t* d_counts, int cap, int P, const int32_t* d_pair_f1,
@@ -2719,17 +2847,42 @@ int orb_search_for_initialization_batch_device(const orb_keypoint_t* d_kps, cons
         return set_err(ORB_EINVAL, "bad arguments");
     if (P == 0) return ORB_OK;
     if (bounds.max_x <= bounds.min_x || bounds.max_y <= bounds.min_y) return set_err(ORB_EINVAL, "bad bounds");
-    const int nmax = std::min(cap, 1024);  // octave-0 keypoints per frame held in LDS
-    if (cap > 8 * nmax) return set_err(ORB_ENOTSUP, "per-frame keypoint capacity too large");
-    size_t lds = match_lds_bytes(cap, nmax);
-    if (lds > 160 * 1024 - 512) return set_err(ORB_ENOTSUP, "per-frame keypoint capacity too large for LDS");
+    if (cap > MATCH_BIG_NMAX) return set_err(ORB_ENOTSUP, "more than 8192 keypoints per frame");
+    const int nmax = std::min(cap, 1024);  // octave-0 keypoints per frame held in LDS by k_match_init
+    const size_t lds = match_lds_bytes(cap, nmax);
+    const int nmaxBig = std::min(cap, MATCH_BIG_NMAX);
+    const size_t ldsBig = match_big_lds_bytes(cap, nmaxBig);
+    if (lds > 159 * 1024 || ldsBig > 159 * 1024)  // 160 KB per CU minus the kernels' static LDS
+        return set_err(ORB_ENOTSUP, "per-frame keypoint capacity too large for LDS");
+    static std::once_flag attrOnce;
+    std::call_once(attrOnce, [] {
+        (void)hipFuncSetAttribute((const void*)k_match_init, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_match_init_big, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  159 * 1024);
+        (void)hipGetLastError();  // an unsupported attribute value must not surface as the launch's error
+    });
     MatchGeom mg{bounds.min_x, bounds.max_x, bounds.min_y, bounds.max_y,
                  static_cast<float>(64) / static_cast<float>(bounds.max_x - bounds.min_x),
                  static_cast<float>(48) / static_cast<float>(bounds.max_y - bounds.min_y)};
-    hipLaunchKernelGGL(k_match_init, dim3(P), dim3(256), lds, (hipStream_t)stream, d_kps, d_desc, d_counts, cap, nmax,
-                       d_pair_f1, d_pair_f2, mg, nnratio, check_ori, (float)window, d_prev_xy, d_matches12,
-                       d_nmatches);
+    MatchArgs A{d_kps, d_desc, d_counts, cap, nmax, d_pair_f1, d_pair_f2, mg, nnratio, check_ori, (float)window,
+                d_prev_xy, d_matches12, d_nmatches, P};
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_match_init, dim3(P), dim3(256), lds, st, A);
     HIP_TRY(hipGetLastError());
+    if (cap > nmax) {
+        // pairs with more than 1024 octave-0 keypoints in a frame (k_match_init left -2) are
+        // redone by the large-capacity kernel; its scratch is stream-ordered
+        const int G = std::min(P, 256);
+        const size_t slot = match_big_slot_bytes(cap, nmaxBig);
+        void* scratch = nullptr;
+        HIP_TRY(hipMallocAsync(&scratch, slot * G, st));
+        A.nmax = nmaxBig;
+        hipLaunchKernelGGL(k_match_init_big, dim3(G), dim3(256), ldsBig, st, A, (uint8_t*)scratch);
+        hipError_t e = hipGetLastError();
+        hipError_t f = hipFreeAsync(scratch, st);
+        if (e != hipSuccess) return set_err(ORB_EDEVICE, std::string("k_match_init_big: ") + hipGetErrorString(e));
+        if (f != hipSuccess) return set_err(ORB_EDEVICE, std::string("hipFreeAsync: ") + hipGetErrorString(f));
+    }
     return ORB_OK;
 }
 
@@ -2744,53 +2897,45 @@ int orb_search_for_initialization(const orb_keypoint_t* kps1, const uint8_t* des
     *n_matches = 0;
     if (n1 == 0) return ORB_OK;
     const int cap = std::max(std::max(n1, n2), 1);
-    if (n1 > 8192 || n2 > 8192) return set_err(ORB_ENOTSUP, "more than 8192 keypoints in a frame");
+    if (n1 > MATCH_BIG_NMAX || n2 > MATCH_BIG_NMAX) return set_err(ORB_ENOTSUP, "more than 8192 keypoints in a frame");
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));
-    orb_keypoint_t* dk = nullptr;
-    uint8_t* dd = nullptr;
-    int *dc = nullptr, *dm = nullptr;
-    float* dp = nullptr;
-    auto cleanup = [&]() {
-        hipFree(dk);
-        hipFree(dd);
-        hipFree(dc);
-        hipFree(dm);
-        hipFree(dp);
-    };
+    // the calling thread's context: grow-only device arena + pinned staging, its own stream
+    // (no per-call allocation, no device-wide synchronisation)
+    OrbHostCtx* C = orb_internal_thread_ctx(dev);
+    if (!C) return set_err(ORB_EINVAL, "device ordinal out of range");
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t oK = 0, oD = oK + al((size_t)2 * cap * sizeof(orb_keypoint_t)), oC = oD + al((size_t)2 * cap * 32),
+                 oP = oC + al(6 * sizeof(int)), oM = oP + al((size_t)cap * 8), total = oM + al((size_t)cap * 4 + 4);
+    if (int r = C->reserve(total, total)) return r;
+    uint8_t* hs = C->pinned;
+    uint8_t* ds = C->buf;
+    std::memcpy(hs + oK, kps1, (size_t)n1 * sizeof(orb_keypoint_t));
+    if (n2) std::memcpy(hs + oK + (size_t)cap * sizeof(orb_keypoint_t), kps2, (size_t)n2 * sizeof(orb_keypoint_t));
+    std::memcpy(hs + oD, desc1, (size_t)n1 * 32);
+    if (n2) std::memcpy(hs + oD + (size_t)cap * 32, desc2, (size_t)n2 * 32);
+    const int hostc[6] = {n1, n2, 0, 1, 0, 0};  // counts of frames 0/1, pair (0, 1)
+    std::memcpy(hs + oC, hostc, sizeof(hostc));
+    std::memcpy(hs + oP, prev_xy, (size_t)n1 * 8);
+    hipStream_t s = C->stream;
+    HIP_TRY(hipMemcpyAsync(ds, hs, oM, hipMemcpyHostToDevice, s));
+    int* dc = (int*)(ds + oC);
+    int* dm = (int*)(ds + oM);
+    int st = orb_search_for_initialization_batch_device((const orb_keypoint_t*)(ds + oK), ds + oD, dc, cap, 1, dc + 2,
+                                                        dc + 3, bounds, nnratio, check_ori, window, (float*)(ds + oP),
+                                                        dm, dm + cap, s);
     hipError_t e = hipSuccess;
-    do {
-        if ((e = hipMalloc(&dk, (size_t)2 * cap * sizeof(orb_keypoint_t))) != hipSuccess) break;
-        if ((e = hipMalloc(&dd, (size_t)2 * cap * 32)) != hipSuccess) break;
-        if ((e = hipMalloc(&dc, 6 * sizeof(int))) != hipSuccess) break;
-        if ((e = hipMalloc(&dm, (size_t)cap * 4 + 4)) != hipSuccess) break;
-        if ((e = hipMalloc(&dp, (size_t)cap * 8)) != hipSuccess) break;
-        int hostc[6] = {n1, n2, 0, 1, 0, 0};
-        if ((e = hipMemcpy(dk, kps1, (size_t)n1 * sizeof(orb_keypoint_t), hipMemcpyHostToDevice)) != hipSuccess) break;
-        if (n2 && (e = hipMemcpy(dk + cap, kps2, (size_t)n2 * sizeof(orb_keypoint_t), hipMemcpyHostToDevice)) != hipSuccess)
-            break;
-        if ((e = hipMemcpy(dd, desc1, (size_t)n1 * 32, hipMemcpyHostToDevice)) != hipSuccess) break;
-        if (n2 && (e = hipMemcpy(dd + (size_t)cap * 32, desc2, (size_t)n2 * 32, hipMemcpyHostToDevice)) != hipSuccess) break;
-        if ((e = hipMemcpy(dc, hostc, sizeof(hostc), hipMemcpyHostToDevice)) != hipSuccess) break;
-        if ((e = hipMemcpy(dp, prev_xy, (size_t)n1 * 8, hipMemcpyHostToDevice)) != hipSuccess) break;
-    } while (0);
-    if (e != hipSuccess) {
-        cleanup();
-        return set_err(ORB_EDEVICE, std::string("match staging: ") + hipGetErrorString(e));
-    }
-    int st = orb_search_for_initialization_batch_device(dk, dd, dc, cap, 1, dc + 2, dc + 3, bounds, nnratio, check_ori,
-                                                        window, dp, dm, dm + cap, nullptr);
-    if (st) {
-        cleanup();
-        return st;
-    }
-    int nm = 0;
-    if ((e = hipDeviceSynchronize()) == hipSuccess && (e = hipMemcpy(matches12, dm, (size_t)n1 * 4, hipMemcpyDeviceToHost)) == hipSuccess &&
-        (e = hipMemcpy(&nm, dm + cap, 4, hipMemcpyDeviceToHost)) == hipSuccess)
-        e = hipMemcpy(prev_xy, dp, (size_t)n1 * 8, hipMemcpyDeviceToHost);
-    cleanup();
+    if (!st) e = hipMemcpyAsync(hs + oP, ds + oP, (size_t)n1 * 8, hipMemcpyDeviceToHost, s);
+    if (!st && e == hipSuccess) e = hipMemcpyAsync(hs + oM, ds + oM, (size_t)cap * 4 + 4, hipMemcpyDeviceToHost, s);
+    hipError_t es = hipStreamSynchronize(s);  // always drained: the staging is reused by the next call
+    if (st) return st;
+    if (e == hipSuccess) e = es;
     if (e != hipSuccess) return set_err(ORB_EDEVICE, std::string("match: ") + hipGetErrorString(e));
-    if (nm < 0) return set_err(ORB_ENOTSUP, "more than 1024 octave-0 keypoints in a frame");
+    int nm = 0;
+    std::memcpy(&nm, hs + oM + (size_t)cap * 4, 4);
+    if (nm < 0) return set_err(ORB_ENOTSUP, "more octave-0 keypoints than the matcher holds");
+    std::memcpy(matches12, hs + oM, (size_t)n1 * 4);
+    std::memcpy(prev_xy, hs + oP, (size_t)n1 * 8);
     *n_matches = nm;
     return ORB_OK;
 }

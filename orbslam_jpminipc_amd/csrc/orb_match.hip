@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <climits>
 #include <cstring>
 #include <mutex>
@@ -874,17 +875,76 @@ __global__ void k_sim3_agree(const int* __restrict__ m1, int n1, const int* __re
 // =========================================================================================
 int fail(int code, const std::string& msg) { return orb_internal_set_error(code, msg); }
 
-// Per-device arena + stream; host entry points are synchronous and serialised per device.
-struct DeviceCtx {
-    std::mutex mu;
-    hipStream_t stream = nullptr;
-    uint8_t* buf = nullptr;
-    size_t cap = 0;
-    uint8_t* pinned = nullptr;  // host staging
-    size_t pcap = 0;
-};
-DeviceCtx g_ctx[64];
+}  // namespace
 
+// ---- per-thread host contexts (orb_internal.h) -------------------------------------------
+int OrbHostCtx::reserve(size_t dev_bytes, size_t host_bytes) {
+    if (!stream) {
+        hipError_t e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking);
+        if (e != hipSuccess) return orb_internal_set_error(ORB_EDEVICE, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+    }
+    if (dev_bytes > cap) {
+        const size_t want = std::max(dev_bytes, cap * 2);
+        if (buf) (void)hipFree(buf);
+        buf = nullptr;
+        cap = 0;
+        hipError_t e = hipMalloc(&buf, want);
+        if (e != hipSuccess) return orb_internal_set_error(ORB_EDEVICE, std::string("hipMalloc: ") + hipGetErrorString(e));
+        cap = want;
+    }
+    if (host_bytes > pcap) {
+        const size_t want = std::max(host_bytes, pcap * 2);
+        if (pinned) (void)hipHostFree(pinned);
+        pinned = nullptr;
+        pcap = 0;
+        hipError_t e = hipHostMalloc((void**)&pinned, want, hipHostMallocDefault);
+        if (e != hipSuccess) return orb_internal_set_error(ORB_EDEVICE, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+        pcap = want;
+    }
+    return ORB_OK;
+}
+
+namespace {
+// Contexts are never destroyed (no HIP teardown at exit); a thread's contexts go back to the
+// pool when it exits.
+struct CtxPool {
+    std::mutex mu;
+    std::vector<OrbHostCtx*> free[64];
+};
+CtxPool& ctx_pool() {
+    static CtxPool* p = new CtxPool();
+    return *p;
+}
+struct ThreadCtxs {
+    OrbHostCtx* c[64] = {};
+    ~ThreadCtxs() {
+        CtxPool& P = ctx_pool();
+        std::lock_guard<std::mutex> lk(P.mu);
+        for (int d = 0; d < 64; ++d)
+            if (c[d]) P.free[d].push_back(c[d]);
+    }
+};
+thread_local ThreadCtxs t_ctxs;
+}  // namespace
+
+OrbHostCtx* orb_internal_thread_ctx(int device) {
+    if (device < 0 || device >= 64) return nullptr;
+    OrbHostCtx*& c = t_ctxs.c[device];
+    if (!c) {
+        CtxPool& P = ctx_pool();
+        std::lock_guard<std::mutex> lk(P.mu);
+        if (!P.free[device].empty()) {
+            c = P.free[device].back();
+            P.free[device].pop_back();
+        } else {
+            c = new OrbHostCtx();
+            c->device = device;
+        }
+    }
+    return c;
+}
+
+namespace {
 // Bump allocator over one device buffer; `stage` copies a host array into it.
 struct Arena {
     std::vector<std::pair<size_t, std::pair<const void*, size_t>>> uploads;
@@ -921,7 +981,7 @@ struct DeviceGuard {
 // A call in flight: the arena layout is planned first (offsets), then allocated + uploaded.
 struct Call {
     int device;
-    DeviceCtx* ctx = nullptr;
+    OrbHostCtx* ctx = nullptr;
     Arena A;
     uint8_t* base = nullptr;
     template <class T>
@@ -932,27 +992,15 @@ struct Call {
         if (device < 0 || device >= 64) return fail(ORB_EINVAL, "bad device ordinal");
         int n = 0;
         if (hipGetDeviceCount(&n) != hipSuccess || device >= n) return fail(ORB_EINVAL, "no such HIP device");
-        ctx = &g_ctx[device];
+        ctx = orb_internal_thread_ctx(device);
         return ORB_OK;
     }
     // allocate (grow) the arena and upload every staged array in one H2D copy
+    std::vector<std::pair<void*, std::pair<size_t, size_t>>> pending;  // (host, (off, bytes)) downloads
+    bool inflight = false;  // work queued on ctx->stream since the last sync()
     int commit() {
-        if (!ctx->stream) HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
-        if (A.size > ctx->cap) {
-            const size_t want = std::max(A.size, ctx->cap * 2);
-            if (ctx->buf) hipFree(ctx->buf);
-            ctx->buf = nullptr;
-            ctx->cap = 0;
-            HIPCHK(hipMalloc(&ctx->buf, want));
-            ctx->cap = want;
-        }
-        if (A.size > ctx->pcap) {
-            if (ctx->pinned) hipHostFree(ctx->pinned);
-            ctx->pinned = nullptr;
-            ctx->pcap = 0;
-            HIPCHK(hipHostMalloc((void**)&ctx->pinned, A.size, hipHostMallocDefault));
-            ctx->pcap = A.size;
-        }
+        if (int st = ctx->reserve(A.size, A.size)) return st;
+        inflight = true;
         base = ctx->buf;
         size_t hi = 0;
         for (auto& u : A.uploads) {
@@ -962,13 +1010,27 @@ struct Call {
         if (hi) HIPCHK(hipMemcpyAsync(base, ctx->pinned, hi, hipMemcpyHostToDevice, ctx->stream));
         return ORB_OK;
     }
+    // D2H through the pinned staging (the arena offset is also the staging offset); the
+    // caller's buffer is filled by sync()
     int download(void* host, size_t off, size_t bytes) {
-        if (bytes) HIPCHK(hipMemcpyAsync(host, base + off, bytes, hipMemcpyDeviceToHost, ctx->stream));
+        inflight = true;
+        if (bytes) {
+            HIPCHK(hipMemcpyAsync(ctx->pinned + off, base + off, bytes, hipMemcpyDeviceToHost, ctx->stream));
+            pending.push_back({host, {off, bytes}});
+        }
         return ORB_OK;
     }
     int sync() {
         HIPCHK(hipStreamSynchronize(ctx->stream));
+        inflight = false;
+        for (auto& d : pending) std::memcpy(d.first, ctx->pinned + d.second.first, d.second.second);
+        pending.clear();
         return ORB_OK;
+    }
+    // an early error return leaves work queued on the context's stream: drain it so the next
+    // call on this thread can reuse the arena and the staging
+    ~Call() {
+        if (inflight) (void)hipStreamSynchronize(ctx->stream);
     }
 };
 
@@ -1075,8 +1137,8 @@ int run_job(const Call& C, const Job& J) {
     size_t lds = 0;
     int st = resolve_lds(J, &lds);
     if (st) return st;
-    static bool attr_set[64] = {};
-    if (!attr_set[C.device]) {
+    static std::atomic<bool> attr_set[64] = {};
+    if (!attr_set[C.device].load()) {
         HIPCHK(hipFuncSetAttribute((const void*)k_resolve, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
         attr_set[C.device] = true;
     }
@@ -1127,7 +1189,6 @@ int bow_match(int mode, const orb_frame_view_t* V1, const uint8_t* flag1, orb_fe
     const int qn = fv1.offsets[fv1.n_nodes];
     Call C{device};
     if ((st = C.begin())) return st;
-    std::lock_guard<std::mutex> lk(C.ctx->mu);
     DeviceGuard dg(device);
     Arena& A = C.A;
     const size_t o1k = A.stage(V1->kps, (size_t)V1->n * sizeof(orb_keypoint_t));
@@ -1206,7 +1267,6 @@ int grid_match(Job J, const orb_frame_view_t* T, const uint8_t* taken, const Gri
     }
     Call C{device};
     if ((st = C.begin())) return st;
-    std::lock_guard<std::mutex> lk(C.ctx->mu);
     DeviceGuard dg(device);
     Arena& A = C.A;
     const ViewOffs vo = plan_view(A, T, true);
@@ -1280,7 +1340,6 @@ int orb_features_in_area(const orb_frame_view_t* view, int keyframe, int q, cons
     }
     Call C{device};
     if ((st = C.begin())) return st;
-    std::lock_guard<std::mutex> lk(C.ctx->mu);
     DeviceGuard dg(device);
     Arena& A = C.A;
     const ViewOffs vo = plan_view(A, view, true);
@@ -1535,7 +1594,6 @@ int orb_search_by_sim3(const orb_frame_view_t* KF1, orb_map_points_t mp1, const 
     // agreement on the device of the call (tiny; keeps the selection off the host)
     Call C{device};
     if ((st = C.begin())) return st;
-    std::lock_guard<std::mutex> lk(C.ctx->mu);
     DeviceGuard dg(device);
     const size_t o1 = C.A.stage(m1.data(), m1.size() * 4), o2 = C.A.stage(m2.data(), m2.size() * 4);
     const size_t oo = C.A.take(std::max<size_t>(m1.size(), 1) * 4), on = C.A.take(16);
@@ -1610,7 +1668,6 @@ extern "C" int orb_frame_is_in_frustum(const orb_frame_view_t* F, orb_map_points
     int st;
     Call C{device};
     if ((st = C.begin())) return st;
-    std::lock_guard<std::mutex> lk(C.ctx->mu);
     DeviceGuard dg(device);
     Arena& A = C.A;
     const size_t n = (size_t)mps.n;

@@ -107,21 +107,45 @@ class ORBextractor:
         """
         import torch
 
+        if d_imgs.dim() != 3:
+            raise TypeError("d_imgs must be a (B, H, W) uint8 device tensor")
         B, h, w = d_imgs.shape
-        cap = self.max_keypoints
-        dev = d_imgs.device
-        if d_kps is None:
-            d_kps = torch.empty((B, cap, 28), dtype=torch.uint8, device=dev)
-        if d_desc is None:
-            d_desc = torch.empty((B, cap, 32), dtype=torch.uint8, device=dev)
-        if d_counts is None:
-            d_counts = torch.empty((B,), dtype=torch.int32, device=dev)
-        s = stream if stream is not None else torch.cuda.current_stream(dev)
+        d_kps, d_desc, d_counts = self._device_io(d_imgs, 1, d_kps, d_desc, d_counts)
+        s = stream if stream is not None else torch.cuda.current_stream(d_imgs.device)
         check(self._lib.orb_extract_batch_device(self._h, B, ptr(d_imgs), w, h, d_imgs.stride(1), d_imgs.stride(0),
                                                  ptr(d_kps), ptr(d_desc), ptr(d_counts),
                                                  ctypes.c_void_p(s.cuda_stream)))
         return d_kps, d_desc, d_counts
 
+
+    def _device_io(self, d_imgs, cn, d_kps, d_desc, d_counts):
+        """Validate a device batch (the C ABI takes raw pointers: a wrong tensor would be
+        silent garbage or out-of-bounds device writes) and allocate missing outputs."""
+        import torch
+
+        B = d_imgs.shape[0]
+        dev = d_imgs.device
+        if dev.type != "cuda" or (dev.index if dev.index is not None else torch.cuda.current_device()) != self.device:
+            raise ValueError(f"d_imgs is on {dev}, the extractor on cuda:{self.device}")
+        if d_imgs.dtype != torch.uint8:
+            raise TypeError("d_imgs must be uint8")
+        if B > self.max_batch:
+            raise ValueError(f"batch {B} exceeds max_batch {self.max_batch}")
+        # pixels of a row contiguous (row pitch = stride(1), frame pitch = stride(0))
+        if (cn == 1 and d_imgs.stride(2) != 1) or (cn > 1 and (d_imgs.stride(3) != 1 or d_imgs.stride(2) != cn)):
+            raise ValueError("image rows must be contiguous")
+        cap = self.max_keypoints
+        outs = []
+        for t, shape in ((d_kps, (B, cap, 28)), (d_desc, (B, cap, 32)), (d_counts, (B,))):
+            dt = torch.int32 if len(shape) == 1 else torch.uint8
+            if t is None:
+                t = torch.empty(shape, dtype=dt, device=dev)
+            elif (t.device != dev or t.dtype != dt or not t.is_contiguous() or t.dim() != len(shape)
+                  or tuple(t.shape[1:]) != shape[1:] or t.shape[0] < B):
+                raise ValueError(f"output tensor must be a contiguous {dt} tensor of shape {shape} (or more "
+                                 f"frames) on {dev}")
+            outs.append(t)
+        return outs
 
     # ---- colour frames: Tracking::GrabImage's cvtColor fused with level 0 (Tracking.cc:202-207)
     def extract_color(self, image, rgb: bool = True):
@@ -147,16 +171,11 @@ class ORBextractor:
         """extract_batch_device on (B, H, W, 3|4) uint8 device frames, converted to gray on the fly."""
         import torch
 
+        if d_imgs.dim() != 4:
+            raise TypeError("d_imgs must be a (B, H, W, 3|4) uint8 device tensor")
         B, h, w, cn = d_imgs.shape
-        cap = self.max_keypoints
-        dev = d_imgs.device
-        if d_kps is None:
-            d_kps = torch.empty((B, cap, 28), dtype=torch.uint8, device=dev)
-        if d_desc is None:
-            d_desc = torch.empty((B, cap, 32), dtype=torch.uint8, device=dev)
-        if d_counts is None:
-            d_counts = torch.empty((B,), dtype=torch.int32, device=dev)
-        s = stream if stream is not None else torch.cuda.current_stream(dev)
+        d_kps, d_desc, d_counts = self._device_io(d_imgs, cn, d_kps, d_desc, d_counts)
+        s = stream if stream is not None else torch.cuda.current_stream(d_imgs.device)
         check(self._lib.orb_extract_batch_device_color(self._h, B, ptr(d_imgs), w, h, d_imgs.stride(1),
                                                        d_imgs.stride(0), cn, int(bool(rgb)), ptr(d_kps), ptr(d_desc),
                                                        ptr(d_counts), ctypes.c_void_p(s.cuda_stream)))

@@ -67,6 +67,17 @@ def sum_over_ranks(value: float, info: DistInfo) -> float:
     return float(t.item())
 
 
+def gather_over_ranks(value: float, info: DistInfo) -> list[float]:
+    """Every rank's scalar, in rank order (the per-rank timed regions of the benchmark)."""
+    if info.world == 1:
+        return [float(value)]
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([float(value)], dtype=torch.float64, device=dev)
+    out = [torch.zeros_like(t) for _ in range(info.world)]
+    dist.all_gather(out, t)
+    return [float(x.item()) for x in out]
+
+
 def whole_job_rate(units_per_rank: int, world: int, seconds_max: float) -> float:
     """Whole-job throughput: all ranks' units over the slowest rank's time (weak scaling)."""
     return units_per_rank * world / seconds_max

@@ -12,11 +12,11 @@ step() {  # step NAME RC
     echo "$1 rc=$2" | tee -a $OUT/summary.txt
     if [ "$2" -ne 0 ] && [ "$2" -ne 1 ]; then echo "abnormal end of $1: stopping" | tee -a $OUT/summary.txt; exit "$2"; fi
 }
-timeout -k 10 600 python -m pytest tests -x -q -m gpu > $OUT/pytest_gpu.log 2>&1
-rc=$?; tail -3 $OUT/pytest_gpu.log >> $OUT/summary.txt; step pytest_gpu $rc
+timeout -k 10 900 python -u -m pytest tests -q -m gpu --maxfail=5 --timeout 180 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
+rc=$?; tail -15 $OUT/pytest_gpu.log >> $OUT/summary.txt; step pytest_gpu $rc
 timeout -k 10 300 python __graft_entry__.py smoke > $OUT/smoke.log 2>&1
 step smoke $?
 timeout -k 10 600 python bench.py "$@" > $OUT/bench.json 2> $OUT/bench.err
 step bench $?
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --cpu-frames 0 "$@" > $OUT/prof.log 2>&1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --cpu-frames 0 --latency 0 "$@" > $OUT/prof.log 2>&1
 step rocprof $?

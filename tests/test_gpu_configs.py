@@ -1,0 +1,195 @@
+"""GPU parity at the benchmark's own scale and under concurrency.
+
+* the bench's timed workload itself (640x480, B = 512 frames of stream 0, 511 consecutive
+  pairs): every frame's keypoints / descriptors and every pair's matches against the oracle;
+* SearchForInitialization past k_match_init's LDS capacity (the reference init extractor at
+  1280x720: nFeatures*2 = 5000, Tracking.cc:126/217) through the batched device entry point;
+* stream ordering of one extractor handle used from two streams, the phase-2
+  guard, and matcher calls from several host threads at once (Tracking / LocalMapping /
+  LoopClosing run matchers concurrently, main.cc:164-193).
+"""
+import threading
+
+import numpy as np
+import pytest
+
+import orbslam_jpminipc_amd as orb
+from oracle_lib import Oracle, OracleMatcher, search_for_initialization
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_extract_all(frames, nf, threads=8):
+    """Oracle extraction of every frame, `threads` oracle instances in parallel (ctypes
+    releases the GIL)."""
+    out = [None] * len(frames)
+
+    def work(t):
+        ora = Oracle(nf, 1.2, 8, 1, 20)
+        for b in range(t, len(frames), threads):
+            out[b] = ora.extract(frames[b])
+
+    ts = [threading.Thread(target=work, args=(t,)) for t in range(threads)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    return out
+
+
+def _device_extract_and_match(frames, nf):
+    import torch
+
+    B, H, W = frames.shape
+    ext = orb.ORBextractor(nf, 1.2, 8, orb.FAST_SCORE, 20, device=0, max_batch=B)
+    d = torch.from_numpy(frames).cuda()
+    kps, desc, cnt = ext.extract_batch_device(d)
+    f1 = torch.arange(0, B - 1, dtype=torch.int32, device="cuda")
+    m12, nm = orb.ORBmatcher(0.9, True).search_for_initialization_batch_device(kps, desc, cnt, f1, f1 + 1, W, H, 100)
+    torch.cuda.synchronize()
+    return kps.cpu().numpy(), desc.cpu().numpy(), cnt.cpu().numpy(), m12.cpu().numpy(), nm.cpu().numpy()
+
+
+def _check_batch(frames, nf, kps, desc, cnt, m12, nm):
+    B, H, W = frames.shape
+    ref = _oracle_extract_all(frames, nf)
+    for b in range(B):
+        ko, do = ref[b]
+        assert cnt[b] == len(ko), b
+        assert kps[b, : cnt[b]].tobytes() == ko.tobytes(), f"frame {b} keypoints"
+        assert desc[b, : cnt[b]].tobytes() == do.tobytes(), f"frame {b} descriptors"
+    for p in range(B - 1):
+        k1, d1 = ref[p]
+        k2, d2 = ref[p + 1]
+        prev = np.ascontiguousarray(np.stack([k1["x"], k1["y"]], 1).astype(np.float32))
+        no, m12o = search_for_initialization(k1, d1, k2, d2, W, H, prev, 0.9, True, 100)
+        assert nm[p] == no, p
+        assert np.array_equal(m12[p, : cnt[p]], m12o), p
+
+
+def test_bench_batch_full_parity():
+    """bench.py's default timed batch, as bench.py builds it (synth_stream(640, 480, stream=rank
+    0, first 0, count 512)): all 512 frames and all 511 pairs bit-exact."""
+    frames = orb.synth_stream(640, 480, stream=0, first=0, count=512)
+    _check_batch(frames, 1000, *_device_extract_and_match(frames, 1000))
+
+
+def test_match_batch_device_over_lds_capacity():
+    """1280x720 with the init extractor's 5000 features: > 1024 octave-0 keypoints per frame,
+    so every pair goes through k_match_init_big."""
+    frames = orb.synth_stream(1280, 720, stream=6, first=0, count=4)
+    kps, desc, cnt, m12, nm = _device_extract_and_match(frames, 5000)
+    oct0 = [int((orb.keypoints_from_bytes(kps[b], cnt[b])["octave"] == 0).sum()) for b in range(len(frames))]
+    assert max(oct0) > 1024, oct0  # the fallback really ran
+    assert (nm > 0).all()
+    _check_batch(frames, 5000, kps, desc, cnt, m12, nm)
+
+
+def test_extractor_two_streams_no_sync():
+    """A device launch on a side stream immediately followed by host-buffer extractions on the
+    same handle (no synchronisation in between): the handle orders its workspace users."""
+    import torch
+
+    B = 4
+    frames = orb.synth_stream(640, 480, stream=12, first=0, count=B)
+    other = orb.synth_stream(640, 480, stream=13, first=0, count=B)
+    ext = orb.ORBextractor(1000, 1.2, 8, orb.FAST_SCORE, 20, device=0, max_batch=B)
+    ref = ext.extract_batch(frames)
+    side = torch.cuda.Stream()
+    d_other = torch.from_numpy(other).cuda()
+    torch.cuda.synchronize()
+    for _ in range(3):
+        with torch.cuda.stream(side):
+            ko, do, co = ext.extract_batch_device(d_other, stream=side)
+        got = ext.extract_batch(frames)  # host entry point, handle stream, no sync before it
+        for b in range(B):
+            assert got[b][0].tobytes() == ref[b][0].tobytes()
+            assert got[b][1].tobytes() == ref[b][1].tobytes()
+        side.synchronize()
+    # and the device result on the side stream is itself intact
+    ora = Oracle(1000, 1.2, 8, 1, 20)
+    c = co.cpu().numpy()
+    for b in range(B):
+        k, d = ora.extract(other[b])
+        assert ko[b, : c[b]].cpu().numpy().tobytes() == k.tobytes()
+
+
+def test_phase2_without_pyramid_rejected():
+    import torch
+
+    ext = orb.ORBextractor(1000, 1.2, 8, orb.FAST_SCORE, 20, device=0, max_batch=4)
+    d = torch.from_numpy(orb.synth_stream(640, 480, stream=1, count=4)).cuda()
+    ext.set_phases(2)
+    with pytest.raises(Exception):
+        ext.extract_batch_device(d)
+    ext.set_phases(1)
+    ext.extract_batch_device(d[:2])
+    ext.set_phases(2)
+    with pytest.raises(Exception):  # pyramid of 2 frames only
+        ext.extract_batch_device(d)
+    ext.extract_batch_device(d[:2])
+    ext.set_phases(3)
+    torch.cuda.synchronize()
+
+
+def test_matchers_from_three_threads():
+    """WindowSearch (Tracking), SearchForTriangulation (LocalMapping) and SearchByBoW KF-KF
+    (LoopClosing) run concurrently from three host threads, plus a fourth running
+    SearchForInitialization; each repeated, each bit-exact against the oracle."""
+    import scenes as S
+    from test_gpu_matcher_family import _bow_pair
+    from orbslam_jpminipc_amd.views import View
+
+    rng = np.random.default_rng(77)
+    F2 = S.view(rng, 1000, clusters=6, spread=20)
+    idx = rng.integers(0, F2.n, 900)
+    k1 = F2.kps[idx].copy()
+    k1["x"] = np.clip(k1["x"] + rng.normal(0, 4, len(idx)), 0, S.W - 1)
+    k1["y"] = np.clip(k1["y"] + rng.normal(0, 4, len(idx)), 0, S.H - 1)
+    F1 = View(k1, S.perturb(rng, F2.desc[idx], 80), (0, S.W, 0, S.H))
+    V1, V2, fv1, fv2 = _bow_pair(rng, n_pts=600, extra=200, share=0.9)
+    F12 = S.fundamental12(V1, V2)
+    h1 = (rng.random(V1.n) < 0.3).astype(np.uint8)
+    h2 = (rng.random(V2.n) < 0.3).astype(np.uint8)
+    u1 = (rng.random(V1.n) < 0.8).astype(np.uint8)
+    u2 = (rng.random(V2.n) < 0.8).astype(np.uint8)
+    frames = orb.synth_stream(640, 480, stream=8, count=2)
+    ext = orb.ORBextractor(1000, 1.2, 8, orb.FAST_SCORE, 20, device=0)
+    Fa, Fb = (orb.Frame.from_image(f, ext) for f in frames)
+    prev0 = np.ascontiguousarray(np.stack([Fa.mvKeys["x"], Fa.mvKeys["y"]], 1).astype(np.float32))
+
+    jobs = {
+        "window": (lambda M: M.WindowSearch(F1, None, F2, 100), 0.9),
+        "triang": (lambda M: M.SearchForTriangulation(V1, h1, fv1, V2, h2, fv2, F12), 0.6),
+        "bow": (lambda M: M.SearchByBoW_KF_KF(V1, u1, fv1, V2, u2, fv2), 0.75),
+    }
+    expect = {k: f(OracleMatcher(nn, True)) for k, (f, nn) in jobs.items()}
+    p = prev0.copy()
+    expect["sfi"] = search_for_initialization(Fa.mvKeys, Fa.mDescriptors, Fb.mvKeys, Fb.mDescriptors, 640, 480, p,
+                                              0.9, True, 100)
+    errors = []
+    start = threading.Barrier(4)
+
+    def run(name):
+        try:
+            start.wait()
+            for _ in range(10):
+                if name == "sfi":
+                    p = prev0.copy()
+                    m12 = []
+                    n = orb.ORBmatcher(0.9, True).SearchForInitialization(Fa, Fb, p, m12, 100)
+                    got = (n, np.array(m12, np.int32))
+                else:
+                    f, nn = jobs[name]
+                    got = f(orb.ORBmatcher(nn, True))
+                ne, oe = expect[name]
+                assert got[0] == ne and np.array_equal(got[1], oe), name
+        except Exception as e:  # reported by the main thread
+            errors.append((name, repr(e)))
+
+    ts = [threading.Thread(target=run, args=(n,)) for n in ("window", "triang", "bow", "sfi")]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errors, errors

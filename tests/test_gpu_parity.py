@@ -210,7 +210,11 @@ def test_phase_split_equals_whole():
         ext.set_phases(4)
 
 
-@pytest.mark.parametrize("W,H,nf", [(640, 480, 1000), (640, 480, 2000), (1241, 376, 2000)])
+# C2/C3, the reference init extractor nFeatures*2 (Tracking.cc:126, 217) at 640x480 / KITTI /
+# 1280x720 (5000 kp: ~1086 level-0 keypoints, over k_match_init's LDS capacity -> the
+# k_match_init_big fallback), C4, C5
+@pytest.mark.parametrize("W,H,nf", [(640, 480, 1000), (640, 480, 2000), (1241, 376, 2000), (1241, 376, 4000),
+                                    (1280, 720, 2500), (1280, 720, 5000)])
 def test_search_for_initialization_parity(W, H, nf):
     ext = orb.ORBextractor(nf, 1.2, 8, orb.FAST_SCORE, 20, device=0)
     frames = orb.synth_stream(W, H, stream=5, first=0, count=4)

@@ -73,3 +73,27 @@ def test_two_rank_replicas_gloo():
     ora = Oracle(300, 1.2, 4, 1, 20)
     for s, c in zip(s0 + s1, c0 + c1):
         assert c == len(ora.extract(orb.synth_stream(160, 120, stream=s, first=0, count=1)[0])[0])
+
+
+def test_bench_launcher_spawns_ranks_dry_run():
+    """`python bench.py --gpus 2` with no launcher around it spawns its two ranks itself (RANK /
+    WORLD_SIZE set before any device call) and prints rank 0's line: n_gpus 2, both ranks'
+    timed regions, value over the slowest.  --dry-run keeps it on the CPU (gloo, oracle)."""
+    import json
+    import pathlib
+    import subprocess
+    import sys
+
+    root = pathlib.Path(__file__).resolve().parent.parent
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, str(root / "bench.py"), "--gpus", "2", "--dry-run", "--steps", "2",
+                        "--warmup", "1"], cwd=root, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr.decode()[-2000:]
+    lines = [l for l in r.stdout.decode().splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2
+    assert len(d["rank_seconds"]) == 2 and all(t > 0 for t in d["rank_seconds"])
+    assert d["value"] == pytest.approx(2 * 2 * 2 / (max(d["rank_seconds"])), rel=0.05)
+    assert d["config"]["parallelism"] == "replicas x2 (no collectives)"
