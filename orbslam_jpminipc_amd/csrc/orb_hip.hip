@@ -35,11 +35,8 @@
 #define ORB_MAX_LEVELS 16
 #define ORB_MAX_CELLS_PER_LEVEL 256
 #define ORB_SELECT_LDS_CAP 6144
-// k_level phase switches: timing experiments only (scripts/klevel_phases.sh builds variants
+// k_fast phase switches: timing experiments only (scripts/klevel_phases.sh builds variants
 // with -DKL_SKIP_*=1 into build/variants); the product build leaves them 0.
-#ifndef KL_SKIP_BLUR
-#define KL_SKIP_BLUR 0
-#endif
 #ifndef KL_SKIP_FAST
 #define KL_SKIP_FAST 0
 #endif
@@ -94,9 +91,10 @@ struct LevelGeom {
     float scale;            // mvScaleFactor[l]
     float size;             // (int)(31 * mvScaleFactor[l])
     int cellW, cellH;       // detection-area size of the (non-last) cells: corner -> cell bucket
+    int cellWm, cellHm;     // ceil(2^32 / cellW), ceil(2^32 / cellH): n / cell = umulhi(n, m), n < 4096
     int detX1, detY1;       // FAST detection region [16, detX1) x [16, detY1): union of the cells' areas
-    int ringX1, ringY1;     // descriptor image defined over [-3, ringX1) x [-3, ringY1): every rBRIEF
-                            // sample (reach 18) of a keypoint in the detection region
+    int ringX1, ringY1;     // rBRIEF samples (reach 18) of detection-region keypoints stay in
+                            // [-3, ringX1) x [-3, ringY1), inside the 16-px padding
 };
 
 struct Geom {
@@ -127,16 +125,6 @@ using namespace orbdev;
 
 __constant__ signed char c_pattern[1024];
 __constant__ float c_patternf[1024];  // the same pattern as floats: lane l's 8 points are 4 float4
-#ifndef KL_COUNT
-#define KL_COUNT 0
-#endif
-#ifndef KL_SKIP_THIN  // timing experiment only: drop tiles with < 64 live columns (wrong output)
-#define KL_SKIP_THIN 0
-#endif
-#if KL_COUNT
-__device__ unsigned long long g_klcount[4];  // lane-rows queued, pixels expanded, corners, survivors
-#endif
-
 // ---- pyramid --------------------------------------------------------------------------
 // Level 0: copyMakeBorder(image, 16, BORDER_REFLECT_101); one thread per 16-byte chunk of a
 // padded row (pitch is a multiple of 16).  Interior chunks (source columns [x-16, x) inside the
@@ -1108,58 +1096,50 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
     if (tid == 0) lvlCount[(long long)b * g.L + l] = keep;
 }
 
-// ---- descriptor image: GaussianBlur(level ROI, 7x7, sigma 2) in place ---------------------
-// The reference blurs the level ROI in place right before its descriptors
-// (ORBextractor.cc:760): samples inside the ROI read the blur, samples in the 16-px padding
-// read the un-blurred reflect-101 border.  k_level materialises exactly that image over level
-// coordinates [-3, ringX1) x [-3, ringY1) (all a keypoint's samples can reach: 3 px past the
-// ROI, more where non-last cells extend past maxBorder) in a buffer laid out like the pyramid.  Fixed-point taps (18,34,49,55,49,34,18)/256 per axis:
-// T = sum_j k_j sum_i k_i P; columns x < 4*floor(w/4) round T/65536 half-to-even (the SSE2
-// SymmColumnVec_32s8u float path), the tail columns half-up ((T + 2^15) >> 16).
-#define BLUR_TW 256  // output columns per tile: 64 lanes x 4 pixels
-#ifndef BLUR_RW
-#define BLUR_RW 9    // output rows per wave: 36-row tiles, 31.5 KB LDS, 5 work-groups per CU (87 VGPRs).
-                     // Measured (640x480, B=256): 8 rows 826 us, 9 rows 734, 12 rows 750.
+// ---- FAST on the levels: per-tile detection + the per-cell non-max suppression --------------
+// ComputeKeyPoints runs cv::FAST(cellImage, keys, fastTh, true) on every cell ROI of every
+// level (ORBextractor.cc:560-607).  A cell's FAST sees its ROI only: detection rows / cols
+// [3, n-3) of the ROI = the cell's detection area, and NMS neighbours outside that area count
+// as 0.  Corner-ness and score are properties of the pixel alone, so one pass
+// over each level's detection region [16, detX1) x [16, detY1) (the union of the cells'
+// areas) finds every cell's corners; the NMS then applies each cell's own boundary.
+//
+// k_fast: one 256-thread workgroup per FT_W x FT_H detection tile of a level, per frame.
+//   (1) stage the tile with its halo (rows y0-4 .. y0+FT_H+3, columns x0-16 .. x0+271) into
+//       LDS with 16-byte loads, all in flight before any LDS write;
+//   (2) per wave, FT_RW rows: compass pre-filter of cv::FAST (a 9-arc always covers two
+//       cyclically adjacent points of {0, 4, 8, 12}) on the lane's 4 pixels, packed 16-bit;
+//       lane-rows with a survivor are queued per wave;
+//   (3) the queue: full 9-arc test at fastTh with one pixel per lane (every lane busy), then
+//       the exact strength S (score = S - 1) of the corners, into an LDS strength plane that
+//       also holds the tile's 1-px halo ring (queued without pre-filter);
+//   (4) after one barrier, the per-cell 3x3 strict NMS from the plane; survivors are appended
+//       to their cell's candidate slots as ((S-1) << 24) | (y << 12) | x (k_select restores
+//       raster order).
+// The 7x7 blur of the descriptors is not materialised: k_orient_desc evaluates it at the
+// rBRIEF sample points from a raw window (ORBextractor.cc:760).
+#define FT_W 256  // detection columns per tile: 64 lanes x 4 pixels
+#ifndef FT_RW
+#define FT_RW 9   // detection rows per wave
 #endif
-#define BLUR_TH (4 * BLUR_RW)  // output rows per tile (4 waves)
-#define BLUR_IW 66   // LDS row pitch in dwords: tile columns x0-4 .. x0+259
-struct BlurTile {
-    int level, x0, y0;  // tile origin in level coordinates: x0 = -4 + 256 k, y0 = -3 + 64 m
+#define FT_H (4 * FT_RW)      // detection rows per tile
+#define FT_IN_P 288           // staged row pitch (bytes): level columns x0-16 .. x0+271 (18 x 16 B)
+#define FT_IN_R (FT_H + 8)    // staged rows y0-4 .. y0+FT_H+3
+#define FT_SPW 264            // strength-plane row pitch (bytes): tile columns -4 .. 259
+#define FT_Q 512              // per-wave queue (u16 entries): lane-rows, then the NMS corner list
+#define FT_CQ 256             // per-wave pixel / corner chunk (u16 entries)
+struct FastTile {
+    int level, x0, y0;  // detection origin in level coordinates: x0 = 16 + 256 k, y0 = 16 + FT_H m
 };
 
-__device__ __forceinline__ int byte_of(uint32_t w, int k) { return (int)((w >> (8 * k)) & 0xFFu); }
-
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef short i16x2 __attribute__((ext_vector_type(2)));
-
-// Gaussian taps (18, 34, 49, 55, 49, 34, 18) = getGaussianKernel(7, 2) in 8-bit fixed point
-// (the host checks its own restatement against these).  Horizontal pass: two
-// v_dot4_u32_u8 per pixel on byte windows [x-3, x] and [x+1, x+4].
-#define GT_WA 0x37312212u  // bytes (x-3, x-2, x-1, x) -> 18, 34, 49, 55
-#define GT_WB 0x00122231u  // bytes (x+1, x+2, x+3, x+4) -> 49, 34, 18, 0
-// Vertical pass in packed fp32 with the 2^-16 output scale folded into the taps: every
-// partial sum is an integer < 2^24 times 2^-16, so the FMAs are exact (only a saturating
-// T >= 2^24 can round, and it clamps to 255 either way).
-#define GV0 (55.0f / 65536.0f)
-#define GV1 (49.0f / 65536.0f)
-#define GV2 (34.0f / 65536.0f)
-#define GV3 (18.0f / 65536.0f)
-
-// Per-wave FAST queue: every lane-row of the wave's rows (and its share of the halo ring)
-// fits, so the queue is drained once, after the row loop.  u16 entry = rowCode << 11 |
-// laneCode << 4 | mask: tile row = wave*BLUR_RW - 1 + rowCode (0..17), bit j of mask is tile
-// column 4*(laneCode-1) + j (laneCode 0 and 65 carry the halo columns -1 and 256).
-#define LVL_FQ ((BLUR_RW + 2) * 64 + 2 * (BLUR_RW + 2))
-#define LVL_CQ 256   // per-wave corner / survivor chunk (u16 entries)
-#define LVL_SPW 264  // LDS strength-plane row pitch (bytes): tile columns -4 .. 259
-
-// Compass pre-filter of cv::FAST (a 9-arc always covers two cyclically adjacent points of
-// {0, 4, 8, 12}) for the 4 pixels of a dword, in packed 16-bit arithmetic: even and odd
-// bytes are split into u16 pairs.  Bright: (q0 > v+t or q8 > v+t) and (q4 or q12 likewise)
-// <=> min(max(q0, q8), max(q4, q12)) > v + t; dark: max(min(q0, q8), min(q4, q12)) < v - t;
-// each comparison is the sign of an i16 difference (all values within i16).  Returns a 4-bit
-// mask (bit j = pixel j passes).
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// Compass pre-filter of cv::FAST for the 4 pixels of a dword, in packed 16-bit arithmetic:
+// even and odd bytes are split into u16 pairs.  Bright: (q0 > v+t or q8 > v+t) and (q4 or q12
+// likewise) <=> min(max(q0, q8), max(q4, q12)) > v + t; dark: max(min(q0, q8), min(q4, q12))
+// < v - t; each comparison is the sign of an i16 difference (all values within i16).
+// Returns a 4-bit mask (bit j = pixel j passes).
 __device__ __forceinline__ uint32_t compass4(uint32_t c, uint32_t q0, uint32_t q4, uint32_t q8, uint32_t q12,
                                              uint32_t tt) {
     uint32_t pass[2];
@@ -1184,177 +1164,71 @@ __device__ __forceinline__ uint32_t compass4(uint32_t c, uint32_t q0, uint32_t q
     return ((pass[0] >> 15) & 1u) | ((pass[1] >> 14) & 2u) | ((pass[0] >> 29) & 4u) | ((pass[1] >> 28) & 8u);
 }
 
-// One tile of one level, four waves of BLUR_RW rows:
-//   (1) the descriptor image rows of the wave (blur: dot4 rows, packed-fp32 columns);
-//   (2) FAST at fastTh inside the detection region [16, detX1) x [16, detY1): compass
-//       pre-filter on the lane's 4 pixels (packed 16-bit), lane-rows with a survivor queued
-//       per wave; the full 9-arc test and the exact strength S run on the queue with all
-//       lanes busy after the row loop, and land in an LDS strength plane, which also holds the
-//       tile's 1-px halo ring (queued without pre-filter);
-//   (3) after one barrier, the per-cell 3x3 NMS of cv::FAST(cellImage, fastTh, true)
-//       (ORBextractor.cc:599-607) from the plane: a corner survives iff S-1 beats the score of
-//       each 8-neighbour inside its cell's detection area (S-1 for a corner, else 0).
-//       Survivors are appended to their cell's candidate slots as ((S-1) << 24) | (y << 12) | x;
-//       cells tile the detection region, so (cell row, col) = ((y-16)/cellH, (x-16)/cellW).
-//       k_select restores raster order.
-__global__ void __launch_bounds__(256) k_level(const uint8_t* __restrict__ pyr, uint8_t* __restrict__ blur, Geom g,
-                                               const BlurTile* __restrict__ tiles, const CellGeom* __restrict__ cells,
-                                               uint32_t* __restrict__ cand, int* __restrict__ cellCount) {
-    __shared__ __attribute__((aligned(16))) uint32_t s_in[(BLUR_TH + 8) * BLUR_IW];
-    __shared__ __attribute__((aligned(16))) uint8_t s_S[(BLUR_TH + 2) * LVL_SPW];
-    __shared__ uint16_t s_pq[4][LVL_FQ];
-    __shared__ uint16_t s_cq[4][LVL_CQ];
-    __shared__ uint16_t s_px[4][LVL_CQ];  // queue entries expanded to pixels (<= 4 x 64)
-    const BlurTile t = tiles[blockIdx.x];
+__global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, Geom g,
+                                              const FastTile* __restrict__ tiles, const CellGeom* __restrict__ cells,
+                                              uint32_t* __restrict__ cand, int* __restrict__ cellCount) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_in[FT_IN_R * FT_IN_P];
+    __shared__ __attribute__((aligned(16))) uint8_t s_S[(FT_H + 2) * FT_SPW];
+    __shared__ uint16_t s_q[4][FT_Q];
+    __shared__ uint16_t s_px[4][FT_CQ];  // a chunk's pixels, compacted in place to its corners
+    const FastTile t = tiles[blockIdx.x];
     const int b = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    // the level's geometry in SGPRs for the whole kernel: read through a reference into the
-    // kernarg block, the compiler re-issued a dependent s_load per use inside the row loop
-    // (12 per row); the empty asm makes the copies opaque, so they cannot be rematerialised
+    // the level's geometry in SGPRs for the whole kernel (read through a reference into the
+    // kernarg block, the compiler re-issued dependent s_loads inside the loops); the empty asm
+    // makes the copies opaque, so they cannot be rematerialised
     LevelGeom lg = g.lv[t.level];
     asm volatile("" : "+s"(lg.w), "+s"(lg.h), "+s"(lg.pitch), "+s"(lg.ph), "+s"(lg.detX1), "+s"(lg.detY1),
-                 "+s"(lg.ringX1), "+s"(lg.ringY1));
-    asm volatile("" : "+s"(lg.xsimd_blur), "+s"(lg.rows), "+s"(lg.cols), "+s"(lg.cellW), "+s"(lg.cellH),
-                 "+s"(lg.cell0), "+s"(lg.base), "+s"(lg.fstride));
-    const uint8_t* src = pyr + lg.base + (long long)b * lg.fstride;
-    uint8_t* dst = blur + lg.base + (long long)b * lg.fstride;
-    // input rows y0-4 .. y0+TH+3 (blur: +-3; FAST ring of a halo pixel: +-4), columns
-    // x0-4 .. x0+259 (padded +16: dword aligned).  Rows past the padded buffer are only needed
-    // by rows that are never written: not loaded.
-    const int py0 = t.y0 - 4 + EDGE, px0 = t.x0 - 4 + EDGE;
-    const int rows = min(BLUR_TH + 8, lg.ph - py0);
-    const int spw = lg.pitch >> 2;
-    stage_rows_to_lds(s_in, BLUR_IW, (const uint32_t*)(src + (long long)py0 * lg.pitch + px0), spw, rows, BLUR_IW,
-                      spw - (px0 >> 2), tid);
-    for (int i = tid; i < (BLUR_TH + 2) * LVL_SPW / 4; i += 256) ((uint32_t*)s_S)[i] = 0u;
+                 "+s"(lg.rows), "+s"(lg.cols));
+    asm volatile("" : "+s"(lg.cellW), "+s"(lg.cellH), "+s"(lg.cellWm), "+s"(lg.cellHm), "+s"(lg.cell0),
+                 "+s"(lg.base), "+s"(lg.fstride));
+    {  // (1) stage: padded rows y0+12 .. (clipped to the buffer), padded columns x0 .. x0+287
+        // (16-byte aligned: x0 = 16 + 256 k and the pitch is a multiple of 16), clipped to the row
+        const uint8_t* src = pyr + lg.base + (long long)b * lg.fstride;
+        const int pr0 = t.y0 - 4 + EDGE;
+        const int rows = min(FT_IN_R, lg.ph - pr0);
+        const int units = min(FT_IN_P / 16, (lg.pitch - t.x0) >> 4);
+        const uint4* gs = (const uint4*)(src + (long long)pr0 * lg.pitch + t.x0);
+        const int gsu = lg.pitch >> 4;
+        constexpr int NU = (FT_IN_R * (FT_IN_P / 16) + 255) / 256;
+        uint4 v[NU];
+#pragma unroll
+        for (int k = 0; k < NU; ++k) {
+            const int i = tid + 256 * k;
+            const int r = i / (FT_IN_P / 16), u = i - r * (FT_IN_P / 16);
+            const bool ok = r < rows && u < units;
+            v[k] = gs[ok ? (long long)r * gsu + u : 0ll];  // every slot loads (no scratch spill)
+            if (!ok) v[k] = make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int k = 0; k < NU; ++k) {
+            const int i = tid + 256 * k;
+            if (i < FT_IN_R * (FT_IN_P / 16)) ((uint4*)s_in)[i] = v[k];
+        }
+        for (int i = tid; i < (FT_H + 2) * FT_SPW / 16; i += 256) ((uint4*)s_S)[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
     __syncthreads();
-    const uint8_t* inb = (const uint8_t*)s_in;
     const int ft = g.fastTh;
     const uint32_t tt = (uint32_t)ft | ((uint32_t)ft << 16);
     const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    uint16_t* pq = s_pq[wave];
-    uint16_t* cq = s_cq[wave];
+    uint16_t* pq = s_q[wave];
     uint16_t* px = s_px[wave];
+    const uint8_t* inb = s_in;
     const int x = t.x0 + 4 * lane;  // first of this lane's 4 columns
-    const int rBase = wave * BLUR_RW - 1;  // tile row of rowCode 0
-    // detection-region columns of this lane (4-bit mask, lane constant)
-    uint32_t colMask = 0;
+    const int rBase = wave * FT_RW - 1;  // tile row of rowCode 0
+    uint32_t colMask = 0;  // detection-region columns of this lane (x >= 16 always)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) colMask |= (uint32_t)(x + j >= EDGE && x + j < lg.detX1) << j;
-    int qn = 0;
-    auto push = [&](uint32_t mask, int rt, int laneCode) {  // wave-uniform call
-        const bool v = mask != 0u;
-        const uint64_t m = __ballot(v);
-        if (v) pq[qn + __popcll(m & below)] = (uint16_t)(((rt - rBase) << 11) | (laneCode << 4) | mask);
-        qn += __popcll(m);
-    };
-    {  // halo ring of the strength plane: rows -1 (wave 0) and TH (wave 3) over the tile's
-       // columns, columns -1 and 256 over rows -1 .. TH (no pre-filter)
-        if (wave == 0 || wave == 3) {
-            const int rt = wave == 0 ? -1 : BLUR_TH;
-            const int Y = t.y0 + rt;
-            push((Y >= EDGE && Y < lg.detY1) ? colMask : 0u, rt, lane + 1);
-        }
-        const int nr = BLUR_RW + (wave == 0) + (wave == 3);  // rows of this wave's column halo
-        const int r0 = wave * BLUR_RW - (wave == 0);
-        const int rt = r0 + (lane >> 1), right = lane & 1;
-        const int X = t.x0 + (right ? BLUR_TW : -1), Y = t.y0 + rt;
-        const bool in = lane < 2 * nr && X >= EDGE && X < lg.detX1 && Y >= EDGE && Y < lg.detY1;
-        push(in ? (right ? 1u : 8u) : 0u, rt, right ? 65 : 0);
-    }
-    const bool colLive = x < lg.ringX1;
-    const bool lanePlain = x >= 0 && x + 3 < lg.xsimd_blur;  // all 4 px inside the ROI, SSE2 columns
-    const uint32_t* in = s_in + (wave * BLUR_RW + 1) * BLUR_IW + lane;
-    f32x2 R[7][2];  // horizontal sums of the ring rows, pixels (0,1) and (2,3)
-    uint32_t C[7];  // centre dwords (x .. x+3) of the ring rows
-    bool done = false;
-    for (int r0 = 0; r0 < BLUR_RW + 6 && !done; r0 += 7) {
-#pragma unroll
-        for (int k = 0; k < 7; ++k) {  // ring slot of row r = r0 + k is k (r0 is a multiple of 7)
-            const int r = r0 + k;
-            if (done || r >= BLUR_RW + 6) break;
-            const uint32_t d0 = in[r * BLUR_IW], d1 = in[r * BLUR_IW + 1], d2 = in[r * BLUR_IW + 2];
-            {
-                const uint32_t h0 = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 1), GT_WA,
-                                                           __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 1), GT_WB, 0u, false), false);
-                const uint32_t h1 = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 2), GT_WA,
-                                                           __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 2), GT_WB, 0u, false), false);
-                const uint32_t h2 = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d1, d0, 3), GT_WA,
-                                                           __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(d2, d1, 3), GT_WB, 0u, false), false);
-                const uint32_t h3 = __builtin_amdgcn_udot4(d1, GT_WA, __builtin_amdgcn_udot4(d2, GT_WB, 0u, false), false);
-                R[k][0] = (f32x2){(float)h0, (float)h1};
-                R[k][1] = (f32x2){(float)h2, (float)h3};
-            }
-            C[k] = d1;
-            if (r < 6) continue;
-            const int rt = wave * BLUR_RW + (r - 6);  // output row (tile); ring slot (k+4)%7 is its centre
-            const int y = t.y0 + rt;
-            if (y >= lg.ringY1) {
-                done = true;
-                break;
-            }
-            const int kc = (k + 4) % 7, km1 = (k + 3) % 7, kp1 = (k + 5) % 7, km2 = (k + 2) % 7, kp2 = (k + 6) % 7,
-                      km3 = (k + 1) % 7;
-            if (colLive && !KL_SKIP_BLUR) {
-                uint32_t word;
-                if (y >= 0 && y < lg.h) {
-                    f32x2 v[2];
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        f32x2 acc = R[kc][h] * (f32x2){GV0, GV0};
-                        acc = __builtin_elementwise_fma(R[km1][h] + R[kp1][h], (f32x2){GV1, GV1}, acc);
-                        acc = __builtin_elementwise_fma(R[km2][h] + R[kp2][h], (f32x2){GV2, GV2}, acc);
-                        acc = __builtin_elementwise_fma(R[km3][h] + R[k][h], (f32x2){GV3, GV3}, acc);
-                        v[h] = acc;
-                    }
-                    const float vv[4] = {v[0].x, v[0].y, v[1].x, v[1].y};
-                    if (lanePlain) {
-                        word = 0u;
-#pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            word = __builtin_amdgcn_cvt_pk_u8_f32(fminf(__builtin_rintf(vv[j]), 255.0f), j, word);
-                    } else {  // ROI edge lanes: raw padding outside, half-up rounding on the tail
-                        const uint32_t craw = C[kc];
-                        word = 0u;
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            const int xj = x + j;
-                            uint32_t bj;
-                            if (xj < 0 || xj >= lg.w) {
-                                bj = (uint32_t)byte_of(craw, j);
-                            } else {
-                                const float rr = xj < lg.xsimd_blur ? __builtin_rintf(vv[j]) : floorf(vv[j] + 0.5f);
-                                bj = (uint32_t)fminf(rr, 255.0f);
-                            }
-                            word |= bj << (8 * j);
-                        }
-                    }
-                } else {
-                    word = C[kc];  // outside the ROI rows: the un-blurred padding
-                }
-                *(uint32_t*)(dst + (long long)(y + EDGE) * lg.pitch + (x + EDGE)) = word;
-            }
-            // FAST pre-filter for the row (wave-uniform row test)
-            if (!KL_SKIP_FAST && y >= EDGE && y < lg.detY1) {
-                const uint32_t cc = C[kc];
-                const uint32_t* ic = in + (r - 3) * BLUR_IW;  // centre row in LDS
-                const uint32_t a4 = __builtin_amdgcn_alignbyte(ic[2], cc, 3);   // x+3 .. x+6
-                const uint32_t a12 = __builtin_amdgcn_alignbyte(cc, ic[0], 1);  // x-3 .. x
-                const uint32_t mask = compass4(cc, C[k], a4, C[km3], a12, tt) & colMask;
-                push(mask, rt, lane + 1);
-            }
-        }
-    }
-    // full 9-arc test + exact strength on the queue, all lanes busy; corners -> plane
-    {
-        const int TP = BLUR_IW * 4;
+    for (int j = 0; j < 4; ++j) colMask |= (uint32_t)(x + j < lg.detX1) << j;
+    // (3) the queue: full 9-arc test + exact strength of pq[0 .. qn), all lanes busy; corners
+    // -> strength plane.  u16 entry = rowCode << 11 | laneCode << 4 | mask: tile row
+    // rBase + rowCode, bit j of mask is tile column 4 * (laneCode - 1) + j (laneCode 0 and 65
+    // carry the halo columns -1 and 256).  Pixel code = (tile row + 1) << 9 | (tile col + 1).
+    auto drain = [&](int qn) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        for (int i0 = 0; i0 < (KL_SKIP_QUEUE ? 0 : qn); i0 += 64) {
+        for (int i0 = 0; i0 < qn; i0 += 64) {
             const int i = i0 + lane;
             const uint32_t e = i < qn ? pq[i] : 0u;
             const int rt = rBase + (int)(e >> 11), cb = 4 * ((int)((e >> 4) & 127) - 1);
-            // expand the 64 lane-row entries into one pixel per slot (order is irrelevant: the
-            // corners land in the strength plane), so the 9-arc test runs with every lane busy
-            int np = 0;
+            int np = 0;  // expand the 64 lane-row entries into one pixel per slot
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const bool v = (e >> j) & 1u;
@@ -1363,43 +1237,73 @@ __global__ void __launch_bounds__(256) k_level(const uint8_t* __restrict__ pyr, 
                 np += __popcll(m);
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#if KL_COUNT
-            if (lane == 0) {
-                atomicAdd(&g_klcount[0], (unsigned long long)min(64, qn - i0));
-                atomicAdd(&g_klcount[1], (unsigned long long)np);
-            }
-#endif
             int cn = 0;
-            for (int p0 = 0; p0 < np; p0 += 64) {
+            for (int p0 = 0; p0 < np; p0 += 64) {  // in-place compaction: writes land at <= p0 + lane
                 bool corner = false;
                 uint16_t c = 0;
                 if (p0 + lane < np) {
                     c = px[p0 + lane];
-                    corner = fast_is_corner(inb + ((c >> 9) + 3) * TP + (c & 511) + 3, TP, ft);
+                    corner = fast_is_corner(inb + ((c >> 9) + 3) * FT_IN_P + (c & 511) + 15, FT_IN_P, ft);
                 }
                 const uint64_t m = __ballot(corner);
-                if (corner) cq[cn + __popcll(m & below)] = c;
+                if (corner) px[cn + __popcll(m & below)] = c;
                 cn += __popcll(m);
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#if KL_COUNT
-            if (lane == 0) atomicAdd(&g_klcount[2], (unsigned long long)cn);
-#endif
             for (int k = lane; k < cn; k += 64) {
-                const uint16_t c = cq[k];
-                const uint8_t* p = inb + ((c >> 9) + 3) * TP + (c & 511) + 3;
-                s_S[(c >> 9) * LVL_SPW + (c & 511) + 3] = (uint8_t)fast_exact_strength(p, TP);
+                const uint16_t c = px[k];
+                const uint8_t* p = inb + ((c >> 9) + 3) * FT_IN_P + (c & 511) + 15;
+                s_S[(c >> 9) * FT_SPW + (c & 511) + 3] = (uint8_t)fast_exact_strength(p, FT_IN_P);
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
+    };
+    int qn = 0;
+    auto push = [&](uint32_t mask, int rt, int laneCode) {  // wave-uniform call
+        const bool v = mask != 0u;
+        const uint64_t m = __ballot(v);
+        if (v) pq[qn + __popcll(m & below)] = (uint16_t)(((rt - rBase) << 11) | (laneCode << 4) | mask);
+        qn += __popcll(m);
+    };
+    {  // halo ring of the strength plane: rows -1 (wave 0) and FT_H (wave 3) over the tile's
+       // columns, columns -1 and 256 over rows -1 .. FT_H (no pre-filter)
+        if (wave == 0 || wave == 3) {
+            const int rt = wave == 0 ? -1 : FT_H;
+            const int Y = t.y0 + rt;
+            push((Y >= EDGE && Y < lg.detY1) ? colMask : 0u, rt, lane + 1);
+        }
+        const int nr = FT_RW + (wave == 0) + (wave == 3);  // rows of this wave's column halo
+        const int r0 = wave * FT_RW - (wave == 0);
+        const int rt = r0 + (lane >> 1), right = lane & 1;
+        const int X = t.x0 + (right ? FT_W : -1), Y = t.y0 + rt;
+        const bool in = lane < 2 * nr && X >= EDGE && X < lg.detX1 && Y >= EDGE && Y < lg.detY1;
+        push(in ? (right ? 1u : 8u) : 0u, rt, right ? 65 : 0);
     }
+    // (2) compass pre-filter, row by row (wave-uniform rows)
+    const uint32_t* in32 = (const uint32_t*)s_in + 4 + lane;  // the lane's centre dword of staged row 0
+    for (int i = 0; i < FT_RW; ++i) {
+        const int rt = wave * FT_RW + i;
+        if (t.y0 + rt >= lg.detY1) break;
+        const uint32_t* row = in32 + (rt + 4) * (FT_IN_P / 4);
+        const uint32_t cc = row[0], lf = row[-1], rg = row[1];
+        const uint32_t up = row[-3 * (FT_IN_P / 4)], dn = row[3 * (FT_IN_P / 4)];
+        const uint32_t a4 = __builtin_amdgcn_alignbyte(rg, cc, 3);   // x+3 .. x+6
+        const uint32_t a12 = __builtin_amdgcn_alignbyte(cc, lf, 1);  // x-3 .. x
+        const uint32_t mask = KL_SKIP_FAST ? 0u : compass4(cc, dn, a4, up, a12, tt) & colMask;
+        if (qn > FT_Q - 64) {
+            if (!KL_SKIP_QUEUE) drain(qn);
+            qn = 0;
+        }
+        push(mask, rt, lane + 1);
+    }
+    if (!KL_SKIP_QUEUE) drain(qn);
     __syncthreads();
-    // (3) in-cell NMS.  Cell (i, j) has the detection area [16 + j*cellW, j == cols-1 ? w-16 :
-    // 16 + (j+1)*cellW) in x (likewise in y), ORBextractor.cc:572-597.
+    // (4) in-cell NMS.  Cell (i, j) has the detection area [16 + j*cellW, j == cols-1 ? w-16 :
+    // 16 + (j+1)*cellW) in x (likewise in y), ORBextractor.cc:572-597; cell of a detection pixel:
+    // ((y-16) / cellH, (x-16) / cellW) by exact reciprocal multiplies (host-checked).
     const CellGeom* lc = cells + lg.cell0;
     int* fcount = cellCount + (long long)b * g.nCells + lg.cell0;
     uint32_t* fcand = cand + (long long)b * g.candPerFrame;
-    // corners of the wave's rows (ballot-compacted from the plane), then the NMS on the list
     int cn = 0;
     auto nms_emit = [&](int n) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1412,11 +1316,12 @@ __global__ void __launch_bounds__(256) k_level(const uint8_t* __restrict__ pyr, 
                 e = pq[k];
                 const int rt = e >> 9, ct = e & 511;
                 const int X = t.x0 + ct, Y = t.y0 + rt;
-                const int ci = (Y - EDGE) / lg.cellH, cj = (X - EDGE) / lg.cellW;
+                const int ci = (int)__umulhi((uint32_t)(Y - EDGE), (uint32_t)lg.cellHm);
+                const int cj = (int)__umulhi((uint32_t)(X - EDGE), (uint32_t)lg.cellWm);
                 if (ci < lg.rows && cj < lg.cols) {
                     const int xlo = EDGE + cj * lg.cellW, xhi = cj == lg.cols - 1 ? lg.w - EDGE : xlo + lg.cellW;
                     const int ylo = EDGE + ci * lg.cellH, yhi = ci == lg.rows - 1 ? lg.h - EDGE : ylo + lg.cellH;
-                    const uint8_t* sp = s_S + (rt + 1) * LVL_SPW + ct + 4;
+                    const uint8_t* sp = s_S + (rt + 1) * FT_SPW + ct + 4;
                     const int S = sp[0];
                     keep = true;
 #pragma unroll
@@ -1425,12 +1330,12 @@ __global__ void __launch_bounds__(256) k_level(const uint8_t* __restrict__ pyr, 
                         for (int dx = -1; dx <= 1; ++dx) {
                             if (dx == 0 && dy == 0) continue;
                             const bool inCell = X + dx >= xlo && X + dx < xhi && Y + dy >= ylo && Y + dy < yhi;
-                            const int nb = inCell ? sp[dy * LVL_SPW + dx] : 0;
+                            const int nb = inCell ? sp[dy * FT_SPW + dx] : 0;
                             keep = keep && (S - 1 > (nb ? nb - 1 : 0));
                         }
                 }
             }
-            // survivors overwrite the front of the chunk (k0 + 64 > sn: no unread entry is hit)
+            // survivors overwrite the front of the list (k0 + 64 > sn: no unread entry is hit)
             const uint64_t m = __ballot(keep);
             if (keep) pq[sn + __popcll(m & below)] = e;
             sn += __popcll(m);
@@ -1440,19 +1345,20 @@ __global__ void __launch_bounds__(256) k_level(const uint8_t* __restrict__ pyr, 
             const uint16_t e = pq[k];
             const int rt = e >> 9, ct = e & 511;
             const int X = t.x0 + ct, Y = t.y0 + rt;
-            const int c = ((Y - EDGE) / lg.cellH) * lg.cols + (X - EDGE) / lg.cellW;
-            const int S = s_S[(rt + 1) * LVL_SPW + ct + 4];
+            const int c = (int)__umulhi((uint32_t)(Y - EDGE), (uint32_t)lg.cellHm) * lg.cols +
+                          (int)__umulhi((uint32_t)(X - EDGE), (uint32_t)lg.cellWm);
+            const int S = s_S[(rt + 1) * FT_SPW + ct + 4];
             const int cap = lc[c].cap, off = lc[c].candOff;
             const int pos = atomicAdd(fcount + c, 1);
             if (pos < cap) fcand[off + pos] = ((uint32_t)(S - 1) << 24) | ((uint32_t)Y << 12) | (uint32_t)X;
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     };
-    for (int i = 0; i < BLUR_RW; ++i) {
-        const int rt = wave * BLUR_RW + i;
-        const int Y = t.y0 + rt;
-        if (Y < EDGE || Y >= lg.detY1) continue;  // wave-uniform
-        const uint32_t w4 = *(const uint32_t*)(s_S + (rt + 1) * LVL_SPW + 4 + 4 * lane);
+    // corners of the wave's rows (ballot-compacted from the plane), then the NMS on the list
+    for (int i = 0; i < FT_RW; ++i) {
+        const int rt = wave * FT_RW + i;
+        if (t.y0 + rt >= lg.detY1) break;  // wave-uniform
+        const uint32_t w4 = *(const uint32_t*)(s_S + (rt + 1) * FT_SPW + 4 + 4 * lane);
         if (__ballot(w4 != 0u) == 0ull) continue;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -1461,7 +1367,7 @@ __global__ void __launch_bounds__(256) k_level(const uint8_t* __restrict__ pyr, 
             if (v) pq[cn + __popcll(m & below)] = (uint16_t)((rt << 9) | (4 * lane + j));
             cn += __popcll(m);
         }
-        if (cn > LVL_FQ - 256) {
+        if (cn > FT_Q - 256) {
             nms_emit(cn);
             cn = 0;
         }
@@ -1471,25 +1377,83 @@ __global__ void __launch_bounds__(256) k_level(const uint8_t* __restrict__ pyr, 
 
 // ---- orientation + descriptor -------------------------------------------------------------
 // One wave per keypoint slot.  Two memory round trips per wave: (1) the slot's packed record
-// and the frame's per-level counts together; (2) the raw 31x31 IC patch and the 37x37 window
-// of the descriptor image that holds every rBRIEF sample (|offset| <= 18)
-// together, both into the wave's own LDS; the angle, sincos and the 512 samples then run
-// from LDS.  No workgroup barrier: a wave reads only what it wrote.
-#define IC_P 36   // LDS pitch of the 31-row IC patch (9 dwords used)
-#define DW_P 40   // LDS pitch of the 37-row descriptor window (10 dwords)
-#define DW_R 18   // window reach
+// and the frame's per-level counts; (2) the raw 43x43 window around the keypoint (rows y-21 ..
+// y+21, 16-byte loads into the wave's own LDS: 64 B per row from the 16-aligned column
+// (x-5) & ~15 of the padded level).  From the window:
+//   * IC_Angle (ORBextractor.cc:124-151) on its raw 31x31 disc;
+//   * the descriptor image the reference reads after GaussianBlur(level ROI, 7x7, sigma 2)
+//     in place (ORBextractor.cc:760), only where rBRIEF samples it: the row pass of the
+//     fixed-point kernel (18, 34, 49, 55, 49, 34, 18) over the window's 44 rows x 40 columns
+//     (x-18 .. x+21) as u16 sums in LDS, rows interleaved in pairs; then per sample the column
+//     pass by four v_dot2 over row pairs, OpenCV's rounding for that column (SSE2 columns
+//     x < 4*floor(w/4) half-to-even, the scalar tail half-up), or the raw
+//     border byte where the sample lies outside the ROI (in-place ROI blur: the padding stays
+//     un-blurred).  Exact integers throughout (T <= 257 * 65535 < 2^24).
+// No workgroup barrier: a wave reads only what it wrote (LDS is in order per wave).
+#define OD_WR 21   // window reach: rBRIEF |offset| <= 18 + the blur's 3
+#define OD_WP 64   // LDS row pitch of the raw window (bytes)
+#define OD_HC 40   // row-pass columns: x-18 .. x+21 (10 groups of 4)
+#define OD_HPR 22  // row pairs of the row-pass sums (window rows 0 .. 43)
+#define GT_WA 0x37312212u  // bytes (x-3, x-2, x-1, x) -> 18, 34, 49, 55
+#define GT_WB 0x00122231u  // bytes (x+1, x+2, x+3, x+4) -> 49, 34, 18, 0
+// column-pass taps over row pairs (low half = the even row): rows r0-3 .. r0+4 when r0 is even
+#define GP_E0 (18u | (34u << 16))
+#define GP_E1 (49u | (55u << 16))
+#define GP_E2 (49u | (34u << 16))
+#define GP_E3 (18u | (0u << 16))
+// ... and rows r0-4 .. r0+3 when r0 is odd (the even row of the first pair is r0-1, tap 0)
+#define GP_O0 (0u | (18u << 16))
+#define GP_O1 (34u | (49u << 16))
+#define GP_O2 (55u | (49u << 16))
+#define GP_O3 (34u | (18u << 16))
 
-__global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__ pyr,
-                                                     const uint8_t* __restrict__ blur, Geom g,
+typedef unsigned short u16x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t dot2u(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2v, a), __builtin_bit_cast(u16x2v, b), c, false);
+}
+
+// Row pass of the 7-tap kernel for 4 consecutive outputs whose 10 input bytes start at byte
+// 0 of (a, b, c) (bytes 0-3, 4-7, 8-11): output j reads bytes j .. j+6.
+__device__ __forceinline__ void hrow4(uint32_t a, uint32_t b, uint32_t c, uint32_t* h) {
+    h[0] = __builtin_amdgcn_udot4(a, GT_WA, __builtin_amdgcn_udot4(b, GT_WB, 0u, false), false);
+    h[1] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(b, a, 1), GT_WA,
+                                  __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(c, b, 1), GT_WB, 0u, false), false);
+    h[2] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(b, a, 2), GT_WA,
+                                  __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(c, b, 2), GT_WB, 0u, false), false);
+    h[3] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(b, a, 3), GT_WA,
+                                  __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(c, b, 3), GT_WB, 0u, false), false);
+}
+
+// Column pass at window column hc (= dx + 18), sums of window rows r0 .. r0+6 (r0 = dy + 18):
+// T = sum_j k_j H(r0 + 3 + j).  Row pairs p0 .. p0+3 hold rows 2 p0 .. 2 p0 + 7; for odd r0 the
+// taps shift by one row (one u16 lane).
+__device__ __forceinline__ uint32_t vpass(const uint32_t* __restrict__ Hs, int r0, int hc) {
+    const int p0 = r0 >> 1;
+    const uint32_t* q = Hs + p0 * OD_HC + hc;
+    const uint32_t h0 = q[0], h1 = q[OD_HC], h2 = q[2 * OD_HC], h3 = q[3 * OD_HC];
+    const bool odd = r0 & 1;
+    const uint32_t t0 = odd ? GP_O0 : GP_E0, t1 = odd ? GP_O1 : GP_E1;
+    const uint32_t t2 = odd ? GP_O2 : GP_E2, t3 = odd ? GP_O3 : GP_E3;
+    return dot2u(h3, t3, dot2u(h2, t2, dot2u(h1, t1, dot2u(h0, t0, 0u))));
+}
+
+// cvRound-equivalent of T / 65536: half to even (SSE2 columns) or half up (scalar tail), then
+// the saturating cast.
+__device__ __forceinline__ uint32_t blur_round(uint32_t T, bool tail) {
+    const uint32_t bias = tail ? 1u : ((T >> 16) & 1u);
+    return min((T + 0x7FFFu + bias) >> 16, 255u);
+}
+
+__global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__ pyr, Geom g,
                                                      const uint32_t* __restrict__ lvlOut,
                                                      const int* __restrict__ lvlCount, orb_keypoint_t* __restrict__ kps,
                                                      uint8_t* __restrict__ desc, int* __restrict__ counts,
                                                      const float* __restrict__ lvlResp) {
-    __shared__ __attribute__((aligned(16))) uint32_t s_patch[4][31 * IC_P / 4];
-    __shared__ __attribute__((aligned(16))) uint32_t s_win[4][(2 * DW_R + 1) * DW_P / 4];
+    __shared__ __attribute__((aligned(16))) uint8_t s_win[4][(2 * OD_WR + 1) * OD_WP];
+    __shared__ __attribute__((aligned(16))) uint32_t s_h[4][OD_HPR * OD_HC];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     // XCD-aware block order: workgroup i runs on XCD i % 8, so give each XCD a contiguous run
-    // of keypoints (neighbouring keypoints share patch rows: L2 hits instead of HBM re-reads)
+    // of keypoints (neighbouring keypoints share window rows: L2 hits instead of HBM re-reads)
     int bid = blockIdx.y * gridDim.x + blockIdx.x;
     const int full = (gridDim.x * gridDim.y) & ~7;
     if (bid < full) bid = (bid & 7) * (full >> 3) + (bid >> 3);
@@ -1500,8 +1464,7 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
         if (k >= g.lv[i].kpBase) l = i;
     const LevelGeom& lg = g.lv[l];
     const int idx = k - lg.kpBase;
-    // wave-uniform record: x, y and the patch bases below live in SGPRs, so every patch load
-    // is SGPR base + 32-bit lane offset (no 64-bit address arithmetic per load)
+    // wave-uniform record: x, y and the window base live in SGPRs
     const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane((int)(k < g.kpCap ? lvlOut[(long long)b * g.kpCap + k] : 0u));
     // output position: level-major order (ORBextractor.cc:749-778)
     int before = 0, cntL = 0, total = 0;
@@ -1514,51 +1477,64 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
     if (k == 0 && lane == 0) counts[b] = total;
     if (k >= g.kpCap || idx >= cntL) return;  // wave-uniform
     const int x = e & 0xFFF, y = (e >> 12) & 0xFFF, score = e >> 24;
-    const long long fbase = lg.base + (long long)b * lg.fstride;
-    const int spw = lg.pitch >> 2;
-    // raw 31x31 patch, rows y-15..y+15, cols x-15..x+15 (dword-aligned spans)
-    const uint8_t* p0 = pyr + fbase + (long long)(y + EDGE - HALF_PATCH) * lg.pitch + (x + EDGE - HALF_PATCH);
-    const int sh = (int)((uintptr_t)p0 & 3);
-    const uint8_t* w0 = p0 - sh;
-    // descriptor window, rows y-18..y+18, cols x-18..x+18 (inside the padded level: x, y lie in
-    // the detection region and ringX1/Y1 <= w/h + 12)
-    const uint8_t* q0 = blur + fbase + (long long)(y + EDGE - DW_R) * lg.pitch + (x + EDGE - DW_R);
-    const int wsh = (int)((uintptr_t)q0 & 3);
-    const uint8_t* v0 = q0 - wsh;
-    uint32_t* P = s_patch[wave];
-    uint32_t* Q = s_win[wave];
-    constexpr int NP = (31 * 9 + 63) / 64, NW = ((2 * DW_R + 1) * 10 + 63) / 64;
-    const uint32_t pitch = (uint32_t)lg.pitch;
-    uint32_t pv[NP], wv[NW];
+    // raw window: padded rows y-5 .. y+37 (level rows y-21 .. y+21), padded columns xa .. xa+63
+    // (inside the padded frame: 16 <= x <= w-7 and y likewise, App. B / DESIGN §4; the last
+    // row's over-read stays inside the pyramid's tail slack)
+    const int xa = (x - 5) & ~15;
+    const uint4* src = (const uint4*)(pyr + lg.base + (long long)b * lg.fstride +
+                                      (long long)(y + EDGE - OD_WR) * lg.pitch + xa);
+    const uint32_t pu = (uint32_t)lg.pitch >> 4;
+    uint8_t* W = s_win[wave];
+    uint32_t* Hs = s_h[wave];
+    {
+        constexpr int NU = (2 * OD_WR + 1) * 4;  // 172 16-byte units
+        uint4 v[3];
 #pragma unroll
-    for (int j = 0; j < NP; ++j) {
-        const int i = lane + 64 * j, r = i / 9, c = i - __mul24(r, 9);
-        pv[j] = i < 31 * 9 ? *(const uint32_t*)(w0 + (__umul24((uint32_t)r, pitch) + 4u * c)) : 0u;
-    }
+        for (int j = 0; j < 3; ++j) {
+            const int i = lane + 64 * j, r = i >> 2, c = i & 3;
+            v[j] = src[i < NU ? __umul24((uint32_t)r, pu) + c : 0u];
+        }
 #pragma unroll
-    for (int j = 0; j < NW; ++j) {
-        const int i = lane + 64 * j, r = i / 10, c = i - __mul24(r, 10);
-        wv[j] = i < (2 * DW_R + 1) * 10 ? *(const uint32_t*)(v0 + (__umul24((uint32_t)r, pitch) + 4u * c)) : 0u;
-    }
-    // LDS rows of 9 (patch) and 10 (window) dwords: the LDS index is the load index itself
-#pragma unroll
-    for (int j = 0; j < NP; ++j) {
-        const int i = lane + 64 * j;
-        if (i < 31 * 9) P[i] = pv[j];
-    }
-#pragma unroll
-    for (int j = 0; j < NW; ++j) {
-        const int i = lane + 64 * j;
-        if (i < (2 * DW_R + 1) * 10) Q[i] = wv[j];
+        for (int j = 0; j < 3; ++j)
+            if (lane + 64 * j < NU) ((uint4*)W)[lane + 64 * j] = v[j];
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS is in order per wave; compiler fence
+    // row pass: task = (row pair, group of 4 columns); window row r = level row y-21+r, sum
+    // column hc = level column x-18+hc; its 7 input bytes start at window byte x-5-xa+hc
+    {
+        const int o0 = x - 5 - xa;  // 0..15, wave-uniform
+        const int sb = o0 & 3, sd = o0 >> 2;
+        const uint32_t* W32 = (const uint32_t*)W;
+        for (int task = lane; task < OD_HPR * (OD_HC / 4); task += 64) {
+            const int rp = task / (OD_HC / 4), gq = task - rp * (OD_HC / 4);
+            uint32_t h[2][4];
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int r = min(2 * rp + s, 2 * OD_WR);  // row 43 pads the last pair (tap 0)
+                // bytes 0 .. 9 of the span (byte 9 lies in d3 when sb == 3)
+                const uint32_t* q = W32 + r * (OD_WP / 4) + gq + sd;
+                const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3];
+                hrow4(__builtin_amdgcn_alignbyte(d1, d0, sb), __builtin_amdgcn_alignbyte(d2, d1, sb),
+                      __builtin_amdgcn_alignbyte(d3, d2, sb), h[s]);
+            }
+            uint4 o;
+            o.x = h[0][0] | (h[1][0] << 16);
+            o.y = h[0][1] | (h[1][1] << 16);
+            o.z = h[0][2] | (h[1][2] << 16);
+            o.w = h[0][3] | (h[1][3] << 16);
+            *(uint4*)(Hs + rp * OD_HC + 4 * gq) = o;
+        }
+    }
     // IC_Angle (ORBextractor.cc:124-151): the disc sums m10 = sum u*I, m01 = sum v*I over
-    // |u| <= umax[|v|], one patch dword per lane and step (unit n = row * 9 + dword: the LDS
-    // index itself).  Byte i of dword c sits at u = base + i, base = 4c - sh - 15, so a dword
-    // adds base * S + sum(i * I_i) to m10 and v * S to m01, S = its in-disc byte sum: two
-    // v_dot4 on the masked dword (integer sums: the same totals in any order).
+    // |u| <= umax[|v|], one patch dword per lane and step (patch row v = window row v + 21,
+    // patch dword c = window dword pd0 + c).  Byte i of dword c sits at u = base + i,
+    // base = 4c - sh - 15, so a dword adds base * S + sum(i * I_i) to m10 and v * S to m01,
+    // S = its in-disc byte sum: two v_dot4 on the masked dword (integer sums: any order).
     int m01 = 0, m10 = 0;
     {
+        const int pc = x + 1 - xa;  // window column of patch column u = -15
+        const int pd0 = pc >> 2, sh = pc & 3;
+        const uint32_t* W32 = (const uint32_t*)W;
         uint64_t umaxNib = 0;  // umax[0..15] as nibbles (wave-uniform)
 #pragma unroll
         for (int i = 0; i < 16; ++i) umaxNib |= (uint64_t)g.umax[i] << (4 * i);
@@ -1572,7 +1548,7 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
                 const int base = 4 * c - sh - HALF_PATCH;
                 const int ilo = max(0, -d - base), ihi = min(3, d - base);
                 const uint32_t mask = ilo > ihi ? 0u : ((0xFFFFFFFFu >> (8 * (3 - ihi))) & (0xFFFFFFFFu << (8 * ilo)));
-                const uint32_t pm = P[n] & mask;
+                const uint32_t pm = W32[(r + OD_WR - HALF_PATCH) * (OD_WP / 4) + pd0 + c] & mask;
                 const int S = (int)__builtin_amdgcn_udot4(pm, 0x01010101u, 0u, false);
                 const int T = (int)__builtin_amdgcn_udot4(pm, 0x03020100u, 0u, false);
                 m10 += __mul24(base, S) + T;  // 24-bit multiplies: full-rate VALU
@@ -1591,8 +1567,6 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
     float sa, ca;
     glibc_sincosf(angle * factorPI, &sa, &ca);
     const float a = ca, bsin = sa;
-    const uint8_t* center = (const uint8_t*)Q + wsh + DW_R * DW_P + DW_R;
-    int vals[8];
     float pat[16];  // pattern points 8*lane .. 8*lane+7 (tests 4*lane .. 4*lane+3): 4 float4 loads
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -1602,12 +1576,23 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
         pat[4 * q + 2] = f.z;
         pat[4 * q + 3] = f.w;
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the row-pass sums are in LDS
+    // wave-uniform: can any sample leave the ROI (raw border bytes) or reach the scalar tail?
+    const bool edge = x - 18 < 0 || x + 18 >= lg.w || y - 18 < 0 || y + 18 >= lg.h;
+    const bool tailAny = x + 18 >= lg.xsimd_blur;
+    int vals[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
         const float px = pat[2 * q], py = pat[2 * q + 1];
         const int dy = (int)rintf(__builtin_fmaf(px, bsin, py * a));
         const int dx = (int)rintf(__builtin_fmaf(px, a, -(py * bsin)));
-        vals[q] = center[__mul24(dy, DW_P) + dx];
+        const uint32_t T = vpass(Hs, dy + OD_WR - 3, dx + 18);
+        uint32_t v = blur_round(T, tailAny && x + dx >= lg.xsimd_blur);
+        if (edge) {
+            const int X = x + dx, Y = y + dy;
+            if (X < 0 || X >= lg.w || Y < 0 || Y >= lg.h) v = W[(dy + OD_WR) * OD_WP + (x + dx + EDGE - xa)];
+        }
+        vals[q] = (int)v;
     }
     int nib = 0;
 #pragma unroll
@@ -1626,6 +1611,30 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
         kp.class_id = -1;
         kps[kslot] = kp;
     }
+}
+
+// The descriptor image of one level (blurred ROI + raw border), over level coordinates
+// [-3, ringX1) x [-3, ringY1), by the same row / column passes and rounding as k_orient_desc:
+// test hook behind orb_debug_blur_image (not on the product path).  One thread per pixel.
+__global__ void __launch_bounds__(256) k_debug_desc_image(const uint8_t* __restrict__ pyr, LevelGeom lg, int b,
+                                                          uint8_t* __restrict__ out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int W = lg.w + 2 * EDGE;
+    const int X = i % W - EDGE, Y = i / W - EDGE;
+    if (Y + EDGE >= lg.h + 2 * EDGE) return;
+    const uint8_t* P = pyr + lg.base + (long long)b * lg.fstride;
+    uint32_t v = P[(long long)(Y + EDGE) * lg.pitch + X + EDGE];
+    if (X >= 0 && X < lg.w && Y >= 0 && Y < lg.h) {
+        uint32_t T = 0;
+        const int kk[7] = {18, 34, 49, 55, 49, 34, 18};
+        for (int j = 0; j < 7; ++j) {
+            uint32_t H = 0;
+            for (int q = 0; q < 7; ++q) H += kk[q] * P[(long long)(Y + j - 3 + EDGE) * lg.pitch + X + q - 3 + EDGE];
+            T += kk[j] * H;
+        }
+        v = blur_round(T, X >= lg.xsimd_blur);
+    }
+    out[i] = (uint8_t)v;
 }
 
 // ---- SearchForInitialization ------------------------------------------------------------
@@ -2105,8 +2114,7 @@ struct orb_extractor {
     size_t tailLds = 0;
     // device workspace
     uint8_t* d_pyr = nullptr;
-    uint8_t* d_blur = nullptr;
-    BlurTile* d_tiles = nullptr;
+    FastTile* d_tiles = nullptr;
     int nTiles = 0;
     uint32_t* d_cand = nullptr;
     int* d_cellCount = nullptr;
@@ -2148,7 +2156,6 @@ struct orb_extractor {
 
     void free_ws() {
         hipFree(d_pyr);
-        hipFree(d_blur);
         hipFree(d_tiles);
         hipFree(d_cand);
         hipFree(d_cellCount);
@@ -2165,7 +2172,6 @@ struct orb_extractor {
         hipFree(d_desc);
         hipFree(d_counts);
         d_pyr = nullptr;
-        d_blur = nullptr;
         d_tiles = nullptr;
         nTiles = 0;
         d_cand = nullptr;
@@ -2273,6 +2279,8 @@ struct orb_extractor {
             lg.nfc = (int)std::ceil((float)nD / nCells);
             lg.cellW = cellW;
             lg.cellH = cellH;
+            lg.cellWm = (int)(uint32_t)((0x100000000ull + cellW - 1) / (uint64_t)cellW);
+            lg.cellHm = (int)(uint32_t)((0x100000000ull + cellH - 1) / (uint64_t)cellH);
             lg.detX1 = std::max(maxBX, levelCols > 1 ? 16 + (levelCols - 1) * cellW : 0);
             lg.detY1 = std::max(maxBY, levelRows > 1 ? 16 + (levelRows - 1) * cellH : 0);
             // keypoints of non-last cells can sit past maxBorder (ORBextractor.cc:560-597); the
@@ -2436,15 +2444,14 @@ struct orb_extractor {
         G.candPerFrame = cand;
         G.kpCap = kpCap;
         // workspace
-        HIP_TRY(hipMalloc(&d_pyr, (size_t)pyrBytes));
-        HIP_TRY(hipMalloc(&d_blur, (size_t)pyrBytes));
-        std::vector<BlurTile> tl;
+        // + slack: k_orient_desc's 64-byte window rows may over-read the last row's pitch
+        HIP_TRY(hipMalloc(&d_pyr, (size_t)pyrBytes + 256));
+        std::vector<FastTile> tl;  // k_fast tiles over each level's detection region
         for (int l = 0; l < nlevels; ++l)
-            for (int y0 = -3; y0 < G.lv[l].ringY1; y0 += BLUR_TH)
-                for (int x0 = -4; x0 < G.lv[l].ringX1; x0 += BLUR_TW)
-                    if (!KL_SKIP_THIN || G.lv[l].ringX1 - x0 >= 64) tl.push_back(BlurTile{l, x0, y0});
-        HIP_TRY(hipMalloc(&d_tiles, tl.size() * sizeof(BlurTile)));
-        HIP_TRY(hipMemcpy(d_tiles, tl.data(), tl.size() * sizeof(BlurTile), hipMemcpyHostToDevice));
+            for (int y0 = orbdev::EDGE; y0 < G.lv[l].detY1; y0 += FT_H)
+                for (int x0 = orbdev::EDGE; x0 < G.lv[l].detX1; x0 += FT_W) tl.push_back(FastTile{l, x0, y0});
+        HIP_TRY(hipMalloc(&d_tiles, tl.size() * sizeof(FastTile)));
+        HIP_TRY(hipMemcpy(d_tiles, tl.data(), tl.size() * sizeof(FastTile), hipMemcpyHostToDevice));
         nTiles = (int)tl.size();
         HIP_TRY(hipMalloc(&d_cand, (size_t)std::max(cand, 1) * maxBatch * 4));
         HIP_TRY(hipMalloc(&d_cellCount, (size_t)G.nCells * maxBatch * 4));
@@ -2575,7 +2582,7 @@ struct orb_extractor {
         }
         stage_begin(2, st);
         HIP_TRY(hipMemsetAsync(d_cellCount, 0, (size_t)g.nCells * B * 4, st));
-        hipLaunchKernelGGL(k_level, dim3(nTiles, B), dim3(256), 0, st, d_pyr, d_blur, g, d_tiles, d_cells, d_cand,
+        hipLaunchKernelGGL(k_fast, dim3(nTiles, B), dim3(256), 0, st, d_pyr, g, d_tiles, d_cells, d_cand,
                            d_cellCount);
         stage_end(2, st);
         stage_begin(3, st);
@@ -2588,8 +2595,8 @@ struct orb_extractor {
         stage_end(3, st);
         stage_begin(4, st);
         dim3 gd((std::max(kpCap, 1) + 3) / 4, B);
-        hipLaunchKernelGGL(k_orient_desc, gd, dim3(256), 0, st, d_pyr, d_blur, g, d_lvl, d_lvlCount, kps, desc,
-                           counts, (const float*)d_lvlResp);
+        hipLaunchKernelGGL(k_orient_desc, gd, dim3(256), 0, st, d_pyr, g, d_lvl, d_lvlCount, kps, desc, counts,
+                           (const float*)d_lvlResp);
         stage_end(4, st);
         HIP_TRY(hipGetLastError());
         return ORB_OK;
@@ -2940,7 +2947,7 @@ int orb_search_for_initialization(const orb_keypoint_t* kps1, const uint8_t* des
     return ORB_OK;
 }
 
-static const char* kStageNames[] = {"k_pyr0", "k_pyr_resize", "k_level", "k_select", "k_orient_desc"};
+static const char* kStageNames[] = {"k_pyr0", "k_pyr_resize", "k_fast", "k_select", "k_orient_desc"};
 
 int orb_profile_enable(orb_extractor_t* h, int enable) {
     return orb_profile_enable_stages(h, enable ? (1u << orb_extractor::kStages) - 1u : 0u);
@@ -3039,29 +3046,29 @@ int orb_debug_level_image(orb_extractor_t* h, int b, int l, uint8_t* out, int* w
     return ORB_OK;
 }
 
-// Descriptor image of level l, frame b (blurred ROI + raw padding ring), padded layout.
+// Descriptor image of level l, frame b (blurred ROI + raw padding), padded layout, computed by
+// k_debug_desc_image with k_orient_desc's rounding (the product never materialises it).
 int orb_debug_blur_image(orb_extractor_t* h, int b, int l, uint8_t* out) {
-    if (!h || l < 0 || l >= h->nlevels || !h->d_blur) return set_err(ORB_EINVAL, "bad arguments");
+    if (!h || l < 0 || l >= h->nlevels || !h->d_pyr || !out) return set_err(ORB_EINVAL, "bad arguments");
     const LevelGeom& lg = h->g.lv[l];
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy2D(out, lg.w + 32, h->d_blur + lg.base + (long long)b * lg.fstride, lg.pitch, lg.w + 32, lg.ph,
-                        hipMemcpyDeviceToHost));
+    const size_t n = (size_t)(lg.w + 32) * (lg.h + 32);
+    uint8_t* d = nullptr;
+    HIP_TRY(hipMalloc(&d, n));
+    hipLaunchKernelGGL(k_debug_desc_image, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, nullptr, h->d_pyr, lg, b, d);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpy(out, d, n, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return set_err(ORB_EDEVICE, std::string("debug descriptor image: ") + hipGetErrorString(e));
     return ORB_OK;
 }
 
 // Per-cell FAST counts (after fallback) of frame `b`, level `l`, row-major cells.
-// k_level queue statistics of a -DKL_COUNT=1 build (timing experiments; 0 otherwise): reads
-// and clears {lane-rows queued, pixels expanded, corners} summed over launches.
+// Retired k_level queue statistics hook (the FAST queue of k_fast is not instrumented): zeros.
 int orb_debug_klevel_counts(unsigned long long* out3) {
-#if KL_COUNT
-    unsigned long long z[4] = {0, 0, 0, 0};
-    HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpyFromSymbol(out3, HIP_SYMBOL(g_klcount), 3 * sizeof(unsigned long long)));
-    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_klcount), z, sizeof(z)));
-#else
+    if (!out3) return set_err(ORB_EINVAL, "bad arguments");
     out3[0] = out3[1] = out3[2] = 0;
-#endif
     return ORB_OK;
 }
 

@@ -2,6 +2,7 @@
 """Per-kernel HBM bytes per launch from the rocprofv3 PMC passes of scripts/pmc_pass.sh.
 
 Usage: pmc_summary.py gpurun_out/TAG [--json OUT] [--width W --height H --batch B --nfeatures N]
+(bench.py reads profiles/pmc_<workload>.json for the roofline's `traffic`)
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch (TCC_EA0 request counters, MI355X_MICROARCH.md
 §HBM).  The guide's ×2 FETCH correction holds for 16-B/lane streaming loads; it is measured in
@@ -27,7 +28,7 @@ def main():
     ap.add_argument("--json")
     ap.add_argument("--width", type=int, default=640)
     ap.add_argument("--height", type=int, default=480)
-    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--batch", type=int, default=512)
     ap.add_argument("--nfeatures", type=int, default=1000)
     ap.add_argument("--dword-factor", type=float, default=1.3532485621757968,
                     help="FETCH_SIZE calibration of dword-per-lane loads: measured on k_pyr0 when it "
