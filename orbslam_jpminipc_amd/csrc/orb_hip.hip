@@ -43,6 +43,18 @@
 #ifndef KL_SKIP_QUEUE
 #define KL_SKIP_QUEUE 0
 #endif
+#ifndef KF_TWO_PASS  // 1: queue = 9-arc test, compaction, then the strength of the corners
+#define KF_TWO_PASS 0
+#endif
+#ifndef KF_TIMING  // 1: per-phase s_memtime sums of k_fast's waves (experiment builds only)
+#define KF_TIMING 0
+#endif
+#if KF_TIMING
+__device__ unsigned long long g_kftime[8];
+#define KF_T(i) const unsigned long long kft##i = __builtin_amdgcn_s_memrealtime()
+#else
+#define KF_T(i)
+#endif
 // k_select ablations (timing-only, likewise): FAST(7) re-run, per-cell and per-level retainBest
 #ifndef KS_SKIP_RERUN
 #define KS_SKIP_RERUN 0
@@ -92,6 +104,8 @@ struct LevelGeom {
     float size;             // (int)(31 * mvScaleFactor[l])
     int cellW, cellH;       // detection-area size of the (non-last) cells: corner -> cell bucket
     int cellWm, cellHm;     // ceil(2^32 / cellW), ceil(2^32 / cellH): n / cell = umulhi(n, m), n < 4096
+    int candBase, capMax;   // cell c of the level owns candidate slots candBase + c * capMax (capMax = the
+                            // level's largest NMS-survivor bound), so k_fast needs no cell table
     int detX1, detY1;       // FAST detection region [16, detX1) x [16, detY1): union of the cells' areas
     int ringX1, ringY1;     // rBRIEF samples (reach 18) of detection-region keypoints stay in
                             // [-3, ringX1) x [-3, ringY1), inside the 16-px padding
@@ -106,6 +120,7 @@ struct Geom {
     int scoreType;
     int taps[4];       // Gaussian 7-tap fixed-point kernel, centre first: 55, 49, 34, 18
     int umax[16];
+    unsigned long long umaxNib;  // umax[0..15] as 4-bit nibbles (k_orient_desc's disc mask)
     LevelGeom lv[ORB_MAX_LEVELS];
 };
 
@@ -125,6 +140,10 @@ using namespace orbdev;
 
 __constant__ signed char c_pattern[1024];
 __constant__ float c_patternf[1024];  // the same pattern as floats: lane l's 8 points are 4 float4
+// IC_Angle disc masks (ORBextractor.cc:124-151 with umax, 495-510) of the 31 x 9 patch dwords for
+// each byte alignment sh of the patch in its dword row: byte i of dword n = 9 r + c is inside the
+// disc iff |4c + i - sh - 15| <= umax[|r - 15|]
+__constant__ uint32_t c_icmask[4 * 288];
 // ---- pyramid --------------------------------------------------------------------------
 // Level 0: copyMakeBorder(image, 16, BORDER_REFLECT_101); one thread per 16-byte chunk of a
 // padded row (pitch is a multiple of 16).  Interior chunks (source columns [x-16, x) inside the
@@ -596,6 +615,39 @@ __device__ __forceinline__ int fast_exact_strength(const uint8_t* p, int TP) {
         B = max(B, mb);
     }
     return max(A, B);
+}
+
+// The same strength with both sides in one packed register: lane 0 of each i16x2 carries the
+// dark contrast v - c, lane 1 the bright contrast c - v; arcs of 9 by doubling windows
+// (2, then 2+2+2+2+1), both sides per instruction.  ~130 VALU and 16 registers of
+// circle values: cheap enough to run on every pre-filter survivor instead of a 9-arc test
+// followed by a second gather for the corners (k_fast's queue is LDS-latency bound).
+typedef short s16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ int fast_strength_packed(const uint8_t* p, int TP) {
+    const int off[16] = {3 * TP, 3 * TP + 1, 2 * TP + 2, TP + 3, 3, -TP + 3, -2 * TP + 2, -3 * TP + 1,
+                         -3 * TP, -3 * TP - 1, -2 * TP - 2, -TP - 3, -3, TP - 3, 2 * TP - 2, 3 * TP - 1};
+    const uint32_t v = p[0];
+    s16x2_t d[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const uint32_t c = p[off[k]];
+        // (v, c) - (c, v) = (v - c, c - v)
+        d[k] = __builtin_bit_cast(s16x2_t, v | (c << 16)) - __builtin_bit_cast(s16x2_t, c | (v << 16));
+    }
+    // windows of 2, then 9 = 2+2+2+2+1 (two register arrays live, not three)
+    s16x2_t m2[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) m2[k] = __builtin_elementwise_min(d[k], d[(k + 1) & 15]);
+    s16x2_t best;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const s16x2_t w9 = __builtin_elementwise_min(
+            __builtin_elementwise_min(__builtin_elementwise_min(m2[k], m2[(k + 2) & 15]),
+                                      __builtin_elementwise_min(m2[(k + 4) & 15], m2[(k + 6) & 15])),
+            d[(k + 8) & 15]);
+        best = k ? __builtin_elementwise_max(best, w9) : w9;
+    }
+    return max((int)best.x, (int)best.y);
 }
 
 // The reference's `FAST(cellImage, keys, 7, true)` re-run of a cell that kept <= 3 corners at
@@ -1164,13 +1216,25 @@ __device__ __forceinline__ uint32_t compass4(uint32_t c, uint32_t q0, uint32_t q
     return ((pass[0] >> 15) & 1u) | ((pass[1] >> 14) & 2u) | ((pass[0] >> 29) & 4u) | ((pass[1] >> 28) & 8u);
 }
 
-__global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, Geom g,
-                                              const FastTile* __restrict__ tiles, const CellGeom* __restrict__ cells,
-                                              uint32_t* __restrict__ cand, int* __restrict__ cellCount) {
+#ifndef KF_NOATOMIC  // timing experiment only (wrong output): survivors stored without the slot atomic
+#define KF_NOATOMIC 0
+#endif
+#ifndef KF_WAVES
+#define KF_WAVES 0  // > 0: waves per SIMD the register allocation targets
+#endif
+#if KF_WAVES
+#define KF_ATTR __attribute__((amdgpu_waves_per_eu(KF_WAVES)))
+#else
+#define KF_ATTR
+#endif
+__global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict__ pyr, Geom g,
+                                                      const FastTile* __restrict__ tiles,
+                                                      uint32_t* __restrict__ cand, int* __restrict__ cellCount) {
     __shared__ __attribute__((aligned(16))) uint8_t s_in[FT_IN_R * FT_IN_P];
     __shared__ __attribute__((aligned(16))) uint8_t s_S[(FT_H + 2) * FT_SPW];
     __shared__ uint16_t s_q[4][FT_Q];
     __shared__ uint16_t s_px[4][FT_CQ];  // a chunk's pixels, compacted in place to its corners
+    KF_T(0);
     const FastTile t = tiles[blockIdx.x];
     const int b = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     // the level's geometry in SGPRs for the whole kernel (read through a reference into the
@@ -1180,7 +1244,7 @@ __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, G
     asm volatile("" : "+s"(lg.w), "+s"(lg.h), "+s"(lg.pitch), "+s"(lg.ph), "+s"(lg.detX1), "+s"(lg.detY1),
                  "+s"(lg.rows), "+s"(lg.cols));
     asm volatile("" : "+s"(lg.cellW), "+s"(lg.cellH), "+s"(lg.cellWm), "+s"(lg.cellHm), "+s"(lg.cell0),
-                 "+s"(lg.base), "+s"(lg.fstride));
+                 "+s"(lg.base), "+s"(lg.fstride), "+s"(lg.candBase), "+s"(lg.capMax));
     {  // (1) stage: padded rows y0+12 .. (clipped to the buffer), padded columns x0 .. x0+287
         // (16-byte aligned: x0 = 16 + 256 k and the pitch is a multiple of 16), clipped to the row
         const uint8_t* src = pyr + lg.base + (long long)b * lg.fstride;
@@ -1207,6 +1271,7 @@ __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, G
         for (int i = tid; i < (FT_H + 2) * FT_SPW / 16; i += 256) ((uint4*)s_S)[i] = make_uint4(0u, 0u, 0u, 0u);
     }
     __syncthreads();
+    KF_T(1);
     const int ft = g.fastTh;
     const uint32_t tt = (uint32_t)ft | ((uint32_t)ft << 16);
     const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -1237,23 +1302,11 @@ __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, G
                 np += __popcll(m);
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            int cn = 0;
-            for (int p0 = 0; p0 < np; p0 += 64) {  // in-place compaction: writes land at <= p0 + lane
-                bool corner = false;
-                uint16_t c = 0;
-                if (p0 + lane < np) {
-                    c = px[p0 + lane];
-                    corner = fast_is_corner(inb + ((c >> 9) + 3) * FT_IN_P + (c & 511) + 15, FT_IN_P, ft);
-                }
-                const uint64_t m = __ballot(corner);
-                if (corner) px[cn + __popcll(m & below)] = c;
-                cn += __popcll(m);
-            }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            for (int k = lane; k < cn; k += 64) {
+            // one pass: the exact strength of every survivor; S > t <=> corner at t
+            for (int k = lane; k < np; k += 64) {
                 const uint16_t c = px[k];
-                const uint8_t* p = inb + ((c >> 9) + 3) * FT_IN_P + (c & 511) + 15;
-                s_S[(c >> 9) * FT_SPW + (c & 511) + 3] = (uint8_t)fast_exact_strength(p, FT_IN_P);
+                const int S = fast_strength_packed(inb + ((c >> 9) + 3) * FT_IN_P + (c & 511) + 15, FT_IN_P);
+                if (S > ft) s_S[(c >> 9) * FT_SPW + (c & 511) + 3] = (uint8_t)S;
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
@@ -1296,14 +1349,16 @@ __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, G
         }
         push(mask, rt, lane + 1);
     }
+    KF_T(2);
     if (!KL_SKIP_QUEUE) drain(qn);
+    KF_T(3);
     __syncthreads();
+    KF_T(4);
     // (4) in-cell NMS.  Cell (i, j) has the detection area [16 + j*cellW, j == cols-1 ? w-16 :
     // 16 + (j+1)*cellW) in x (likewise in y), ORBextractor.cc:572-597; cell of a detection pixel:
     // ((y-16) / cellH, (x-16) / cellW) by exact reciprocal multiplies (host-checked).
-    const CellGeom* lc = cells + lg.cell0;
     int* fcount = cellCount + (long long)b * g.nCells + lg.cell0;
-    uint32_t* fcand = cand + (long long)b * g.candPerFrame;
+    uint32_t* fcand = cand + (long long)b * g.candPerFrame + lg.candBase;
     int cn = 0;
     auto nms_emit = [&](int n) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1348,9 +1403,9 @@ __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, G
             const int c = (int)__umulhi((uint32_t)(Y - EDGE), (uint32_t)lg.cellHm) * lg.cols +
                           (int)__umulhi((uint32_t)(X - EDGE), (uint32_t)lg.cellWm);
             const int S = s_S[(rt + 1) * FT_SPW + ct + 4];
-            const int cap = lc[c].cap, off = lc[c].candOff;
-            const int pos = atomicAdd(fcount + c, 1);
-            if (pos < cap) fcand[off + pos] = ((uint32_t)(S - 1) << 24) | ((uint32_t)Y << 12) | (uint32_t)X;
+            const int pos = KF_NOATOMIC ? k : atomicAdd(fcount + c, 1);
+            if (pos < lg.capMax)
+                fcand[c * lg.capMax + pos] = ((uint32_t)(S - 1) << 24) | ((uint32_t)Y << 12) | (uint32_t)X;
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     };
@@ -1373,6 +1428,17 @@ __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, G
         }
     }
     if (cn) nms_emit(cn);
+#if KF_TIMING
+    KF_T(5);
+    if (lane == 0) {
+        atomicAdd(&g_kftime[0], kft1 - kft0);
+        atomicAdd(&g_kftime[1], kft2 - kft1);
+        atomicAdd(&g_kftime[2], kft3 - kft2);
+        atomicAdd(&g_kftime[3], kft4 - kft3);
+        atomicAdd(&g_kftime[4], kft5 - kft4);
+        atomicAdd(&g_kftime[5], 1ull);
+    }
+#endif
 }
 
 // ---- orientation + descriptor -------------------------------------------------------------
@@ -1499,30 +1565,34 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
             if (lane + 64 * j < NU) ((uint4*)W)[lane + 64 * j] = v[j];
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS is in order per wave; compiler fence
-    // row pass: task = (row pair, group of 4 columns); window row r = level row y-21+r, sum
-    // column hc = level column x-18+hc; its 7 input bytes start at window byte x-5-xa+hc
+    // row pass: task = (4 window rows = 2 row pairs, group of 4 columns); window row r = level row
+    // y-21+r, sum column hc = level column x-18+hc; its 7 input bytes start at window byte
+    // x-5-xa+hc
     {
         const int o0 = x - 5 - xa;  // 0..15, wave-uniform
         const int sb = o0 & 3, sd = o0 >> 2;
         const uint32_t* W32 = (const uint32_t*)W;
-        for (int task = lane; task < OD_HPR * (OD_HC / 4); task += 64) {
-            const int rp = task / (OD_HC / 4), gq = task - rp * (OD_HC / 4);
-            uint32_t h[2][4];
+        for (int task = lane; task < (OD_HPR / 2) * (OD_HC / 4); task += 64) {
+            const int rq = task / (OD_HC / 4), gq = task - rq * (OD_HC / 4);
+            uint32_t h[4][4];
 #pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                const int r = min(2 * rp + s, 2 * OD_WR);  // row 43 pads the last pair (tap 0)
+            for (int s2 = 0; s2 < 4; ++s2) {
+                const int r = min(4 * rq + s2, 2 * OD_WR);  // row 43 pads the last pair (tap 0)
                 // bytes 0 .. 9 of the span (byte 9 lies in d3 when sb == 3)
                 const uint32_t* q = W32 + r * (OD_WP / 4) + gq + sd;
                 const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3];
                 hrow4(__builtin_amdgcn_alignbyte(d1, d0, sb), __builtin_amdgcn_alignbyte(d2, d1, sb),
-                      __builtin_amdgcn_alignbyte(d3, d2, sb), h[s]);
+                      __builtin_amdgcn_alignbyte(d3, d2, sb), h[s2]);
             }
-            uint4 o;
-            o.x = h[0][0] | (h[1][0] << 16);
-            o.y = h[0][1] | (h[1][1] << 16);
-            o.z = h[0][2] | (h[1][2] << 16);
-            o.w = h[0][3] | (h[1][3] << 16);
-            *(uint4*)(Hs + rp * OD_HC + 4 * gq) = o;
+#pragma unroll
+            for (int pr = 0; pr < 2; ++pr) {
+                uint4 o;
+                o.x = h[2 * pr][0] | (h[2 * pr + 1][0] << 16);
+                o.y = h[2 * pr][1] | (h[2 * pr + 1][1] << 16);
+                o.z = h[2 * pr][2] | (h[2 * pr + 1][2] << 16);
+                o.w = h[2 * pr][3] | (h[2 * pr + 1][3] << 16);
+                *(uint4*)(Hs + (2 * rq + pr) * OD_HC + 4 * gq) = o;
+            }
         }
     }
     // IC_Angle (ORBextractor.cc:124-151): the disc sums m10 = sum u*I, m01 = sum v*I over
@@ -1535,24 +1605,17 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
         const int pc = x + 1 - xa;  // window column of patch column u = -15
         const int pd0 = pc >> 2, sh = pc & 3;
         const uint32_t* W32 = (const uint32_t*)W;
-        uint64_t umaxNib = 0;  // umax[0..15] as nibbles (wave-uniform)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) umaxNib |= (uint64_t)g.umax[i] << (4 * i);
+        const uint32_t* mt = c_icmask + 288 * sh;
 #pragma unroll
         for (int j = 0; j < (31 * 9 + 63) / 64; ++j) {
             const int n = lane + 64 * j;
             if (n < 31 * 9) {
                 const int r = n / 9, c = n - r * 9;
-                const int v = r - HALF_PATCH;
-                const int d = (int)(umaxNib >> (4 * (v < 0 ? -v : v))) & 15;
-                const int base = 4 * c - sh - HALF_PATCH;
-                const int ilo = max(0, -d - base), ihi = min(3, d - base);
-                const uint32_t mask = ilo > ihi ? 0u : ((0xFFFFFFFFu >> (8 * (3 - ihi))) & (0xFFFFFFFFu << (8 * ilo)));
-                const uint32_t pm = W32[(r + OD_WR - HALF_PATCH) * (OD_WP / 4) + pd0 + c] & mask;
+                const uint32_t pm = W32[(r + OD_WR - HALF_PATCH) * (OD_WP / 4) + pd0 + c] & mt[n];
                 const int S = (int)__builtin_amdgcn_udot4(pm, 0x01010101u, 0u, false);
                 const int T = (int)__builtin_amdgcn_udot4(pm, 0x03020100u, 0u, false);
-                m10 += __mul24(base, S) + T;  // 24-bit multiplies: full-rate VALU
-                m01 += __mul24(v, S);
+                m10 += __mul24(4 * c - sh - HALF_PATCH, S) + T;  // 24-bit multiplies: full-rate VALU
+                m01 += __mul24(r - HALF_PATCH, S);
             }
         }
     }
@@ -2234,6 +2297,8 @@ struct orb_extractor {
         if (G.taps[0] != 55 || G.taps[1] != 49 || G.taps[2] != 34 || G.taps[3] != 18)
             return set_err(ORB_EINVAL, "Gaussian taps differ from the kernel's constants (GT_WA/GT_WB)");
         for (int v = 0; v < 16; ++v) G.umax[v] = umax[v];
+        G.umaxNib = 0;
+        for (int v = 0; v < 16; ++v) G.umaxNib |= (unsigned long long)umax[v] << (4 * v);
         std::vector<CellGeom> cl;
         std::vector<int> rt;
         long long pyrBytes = 0;
@@ -2334,11 +2399,16 @@ struct orb_extractor {
                             cellLds = std::max(cellLds, lds);
                         }
                     }
-                    c.candOff = cand;
-                    cand += c.cap;
                     cl.push_back(c);
                 }
             }
+            // uniform slot stride per level (k_fast computes a cell's slots arithmetically)
+            int capMax = 0;
+            for (size_t i = lg.cell0; i < cl.size(); ++i) capMax = std::max(capMax, cl[i].cap);
+            lg.candBase = cand;
+            lg.capMax = capMax;
+            for (size_t i = lg.cell0; i < cl.size(); ++i) cl[i].candOff = cand + (int)(i - lg.cell0) * capMax;
+            cand += (int)(cl.size() - lg.cell0) * capMax;
         }
         selectLds = std::max(cellLds, (size_t)(scoreType == ORB_HARRIS_SCORE ? 4 : 2) * SELECT_CAP * 4);
         if (selectLds > 150 * 1024) return set_err(ORB_ENOTSUP, "FAST cell larger than the LDS budget");
@@ -2453,6 +2523,7 @@ struct orb_extractor {
         HIP_TRY(hipMalloc(&d_tiles, tl.size() * sizeof(FastTile)));
         HIP_TRY(hipMemcpy(d_tiles, tl.data(), tl.size() * sizeof(FastTile), hipMemcpyHostToDevice));
         nTiles = (int)tl.size();
+
         HIP_TRY(hipMalloc(&d_cand, (size_t)std::max(cand, 1) * maxBatch * 4));
         HIP_TRY(hipMalloc(&d_cellCount, (size_t)G.nCells * maxBatch * 4));
         HIP_TRY(hipMalloc(&d_cand2, (size_t)std::max(cand, 1) * maxBatch * 4));
@@ -2582,8 +2653,7 @@ struct orb_extractor {
         }
         stage_begin(2, st);
         HIP_TRY(hipMemsetAsync(d_cellCount, 0, (size_t)g.nCells * B * 4, st));
-        hipLaunchKernelGGL(k_fast, dim3(nTiles, B), dim3(256), 0, st, d_pyr, g, d_tiles, d_cells, d_cand,
-                           d_cellCount);
+        hipLaunchKernelGGL(k_fast, dim3(nTiles, B), dim3(256), 0, st, d_pyr, g, d_tiles, d_cand, d_cellCount);
         stage_end(2, st);
         stage_begin(3, st);
         if (scoreType == ORB_HARRIS_SCORE)
@@ -2612,6 +2682,26 @@ static int upload_pattern(int device) {
     float pf[1024];
     for (int i = 0; i < 1024; ++i) pf[i] = (float)kOrbPattern31[i];
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_patternf), pf, sizeof(pf)));
+    {  // IC disc masks per alignment (umax of ORBextractor.cc:495-510, HALF_PATCH_SIZE 15)
+        int um[16];
+        const int vmax = (int)std::floor(15 * std::sqrt(2.f) / 2 + 1), vmin = (int)std::ceil(15 * std::sqrt(2.f) / 2);
+        for (int v = 0; v <= vmax; ++v) um[v] = (int)lrint(std::sqrt(225.0 - v * v));
+        for (int v = 15, v0 = 0; v >= vmin; --v) {
+            while (um[v0] == um[v0 + 1]) ++v0;
+            um[v] = v0;
+            ++v0;
+        }
+        uint32_t mt[4 * 288] = {};
+        for (int sh = 0; sh < 4; ++sh)
+            for (int n = 0; n < 31 * 9; ++n) {
+                const int r = n / 9, c = n % 9, v = std::abs(r - 15);
+                uint32_t m = 0;
+                for (int i = 0; i < 4; ++i)
+                    if (std::abs(4 * c + i - sh - 15) <= um[v]) m |= 0xFFu << (8 * i);
+                mt[288 * sh + n] = m;
+            }
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_icmask), mt, sizeof(mt)));
+    }
     if (device >= 0 && device < 64) uploaded[device] = true;
     return ORB_OK;
 }
@@ -3065,6 +3155,16 @@ int orb_debug_blur_image(orb_extractor_t* h, int b, int l, uint8_t* out) {
 }
 
 // Per-cell FAST counts (after fallback) of frame `b`, level `l`, row-major cells.
+#if KF_TIMING
+// experiment builds: k_fast's per-phase s_memtime sums {stage, rows, drain, barrier, nms, waves}
+int orb_debug_kf_timing(unsigned long long* out6) {
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out6, HIP_SYMBOL(g_kftime), 6 * sizeof(unsigned long long)));
+    unsigned long long z[8] = {};
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_kftime), z, sizeof(z)));
+    return ORB_OK;
+}
+#endif
 // Retired k_level queue statistics hook (the FAST queue of k_fast is not instrumented): zeros.
 int orb_debug_klevel_counts(unsigned long long* out3) {
     if (!out3) return set_err(ORB_EINVAL, "bad arguments");
