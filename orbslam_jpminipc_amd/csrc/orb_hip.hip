@@ -1179,7 +1179,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
 #define FT_IN_R (FT_H + 8)    // staged rows y0-4 .. y0+FT_H+3
 #define FT_SPW 264            // strength-plane row pitch (bytes): tile columns -4 .. 259
 #define FT_Q 512              // per-wave queue (u16 entries): lane-rows, then the NMS corner list
-#define FT_CQ 256             // per-wave pixel / corner chunk (u16 entries)
+#define FT_CQ 320             // per-wave pixel list (u16 entries): < 64 carried + 256 expanded
 struct FastTile {
     int level, x0, y0;  // detection origin in level coordinates: x0 = 16 + 256 k, y0 = 16 + FT_H m
 };
@@ -1232,8 +1232,10 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
                                                       uint32_t* __restrict__ cand, int* __restrict__ cellCount) {
     __shared__ __attribute__((aligned(16))) uint8_t s_in[FT_IN_R * FT_IN_P];
     __shared__ __attribute__((aligned(16))) uint8_t s_S[(FT_H + 2) * FT_SPW];
-    __shared__ uint16_t s_q[4][FT_Q];
-    __shared__ uint16_t s_px[4][FT_CQ];  // a chunk's pixels, compacted in place to its corners
+    // per-wave lists; the last slot of each is a trash slot, so ballot-compacted appends store
+    // unconditionally (no exec-mask branch per append)
+    __shared__ uint16_t s_q[4][FT_Q + 2];
+    __shared__ uint16_t s_px[4][FT_CQ + 2];  // a chunk's pixels, compacted in place to its corners
     KF_T(0);
     const FastTile t = tiles[blockIdx.x];
     const int b = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1287,35 +1289,44 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
     // -> strength plane.  u16 entry = rowCode << 11 | laneCode << 4 | mask: tile row
     // rBase + rowCode, bit j of mask is tile column 4 * (laneCode - 1) + j (laneCode 0 and 65
     // carry the halo columns -1 and 256).  Pixel code = (tile row + 1) << 9 | (tile col + 1).
+    // pixels expanded from the queue wait in px until a full pass of 64 is ready (partial
+    // passes only at the very end), so the strength passes run with every lane busy
+    int np = 0;
+    auto strength_pass = [&](int base, int n) {  // px[base .. base + n), n <= 64
+        if (lane < n) {
+            const uint16_t c = px[base + lane];
+            const int S = fast_strength_packed(inb + ((c >> 9) + 3) * FT_IN_P + (c & 511) + 15, FT_IN_P);
+            s_S[(c >> 9) * FT_SPW + (c & 511) + 3] = (uint8_t)(S > ft ? S : 0);  // each pixel once
+        }
+    };
     auto drain = [&](int qn) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         for (int i0 = 0; i0 < qn; i0 += 64) {
             const int i = i0 + lane;
             const uint32_t e = i < qn ? pq[i] : 0u;
             const int rt = rBase + (int)(e >> 11), cb = 4 * ((int)((e >> 4) & 127) - 1);
-            int np = 0;  // expand the 64 lane-row entries into one pixel per slot
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < 4; ++j) {  // expand the 64 lane-row entries into one pixel per slot
                 const bool v = (e >> j) & 1u;
                 const uint64_t m = __ballot(v);
-                if (v) px[np + __popcll(m & below)] = (uint16_t)(((rt + 1) << 9) | (cb + j + 1));
+                px[v ? np + __popcll(m & below) : FT_CQ] = (uint16_t)(((rt + 1) << 9) | (cb + j + 1));
                 np += __popcll(m);
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            // one pass: the exact strength of every survivor; S > t <=> corner at t
-            for (int k = lane; k < np; k += 64) {
-                const uint16_t c = px[k];
-                const int S = fast_strength_packed(inb + ((c >> 9) + 3) * FT_IN_P + (c & 511) + 15, FT_IN_P);
-                if (S > ft) s_S[(c >> 9) * FT_SPW + (c & 511) + 3] = (uint8_t)S;
+            // full passes from the top of the list (the next expansion overwrites what they read:
+            // LDS accesses of one wave complete in issue order)
+            while (np >= 64) {
+                np -= 64;
+                strength_pass(np, 64);
             }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     };
     int qn = 0;
     auto push = [&](uint32_t mask, int rt, int laneCode) {  // wave-uniform call
         const bool v = mask != 0u;
         const uint64_t m = __ballot(v);
-        if (v) pq[qn + __popcll(m & below)] = (uint16_t)(((rt - rBase) << 11) | (laneCode << 4) | mask);
+        pq[v ? qn + __popcll(m & below) : FT_Q] = (uint16_t)(((rt - rBase) << 11) | (laneCode << 4) | mask);
         qn += __popcll(m);
     };
     {  // halo ring of the strength plane: rows -1 (wave 0) and FT_H (wave 3) over the tile's
@@ -1350,7 +1361,10 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
         push(mask, rt, lane + 1);
     }
     KF_T(2);
-    if (!KL_SKIP_QUEUE) drain(qn);
+    if (!KL_SKIP_QUEUE) {
+        drain(qn);
+        if (np) strength_pass(0, np);  // the remainder, < 64 pixels
+    }
     KF_T(3);
     __syncthreads();
     KF_T(4);
@@ -1376,23 +1390,32 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
                 if (ci < lg.rows && cj < lg.cols) {
                     const int xlo = EDGE + cj * lg.cellW, xhi = cj == lg.cols - 1 ? lg.w - EDGE : xlo + lg.cellW;
                     const int ylo = EDGE + ci * lg.cellH, yhi = ci == lg.rows - 1 ? lg.h - EDGE : ylo + lg.cellH;
+                    // the plane holds the tile's 1-px ring, so all 9 reads are in bounds: issue
+                    // them together (no per-neighbour branch), then mask the out-of-cell ones
                     const uint8_t* sp = s_S + (rt + 1) * FT_SPW + ct + 4;
-                    const int S = sp[0];
-                    keep = true;
+                    int nbv[9];
+#pragma unroll
+                    for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+                        for (int dx = -1; dx <= 1; ++dx) nbv[(dy + 1) * 3 + dx + 1] = sp[dy * FT_SPW + dx];
+                    const int S = nbv[4];
+                    const bool xl = X - 1 >= xlo, xr = X + 1 < xhi, yu = Y - 1 >= ylo, yd = Y + 1 < yhi;
+                    bool ok = true;
 #pragma unroll
                     for (int dy = -1; dy <= 1; ++dy)
 #pragma unroll
                         for (int dx = -1; dx <= 1; ++dx) {
                             if (dx == 0 && dy == 0) continue;
-                            const bool inCell = X + dx >= xlo && X + dx < xhi && Y + dy >= ylo && Y + dy < yhi;
-                            const int nb = inCell ? sp[dy * FT_SPW + dx] : 0;
-                            keep = keep && (S - 1 > (nb ? nb - 1 : 0));
+                            const bool inCell = (dx < 0 ? xl : dx > 0 ? xr : true) & (dy < 0 ? yu : dy > 0 ? yd : true);
+                            const int nb = inCell ? nbv[(dy + 1) * 3 + dx + 1] : 0;
+                            ok &= S - 1 > (nb ? nb - 1 : 0);
                         }
+                    keep = ok;
                 }
             }
             // survivors overwrite the front of the list (k0 + 64 > sn: no unread entry is hit)
             const uint64_t m = __ballot(keep);
-            if (keep) pq[sn + __popcll(m & below)] = e;
+            pq[keep ? sn + __popcll(m & below) : FT_Q] = e;
             sn += __popcll(m);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1419,7 +1442,7 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
         for (int j = 0; j < 4; ++j) {
             const bool v = ((w4 >> (8 * j)) & 0xFFu) != 0u;
             const uint64_t m = __ballot(v);
-            if (v) pq[cn + __popcll(m & below)] = (uint16_t)((rt << 9) | (4 * lane + j));
+            pq[v ? cn + __popcll(m & below) : FT_Q] = (uint16_t)((rt << 9) | (4 * lane + j));
             cn += __popcll(m);
         }
         if (cn > FT_Q - 256) {
