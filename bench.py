@@ -88,14 +88,14 @@ def stage_bytes(W, H, n_kp, B):
     B_ext = sum_l w_l h_l (each level read once) + sum_{l>=1} w_l h_l (each derived level
     written once) + 60 N_kp (keypoint + descriptor records written), split over the stages
     that carry each term: the level-0 input read by k_pyr0, the derived levels written by the
-    resize stage (per launch: per level), every level read by k_level (detection), the records
+    resize stage (per launch: per level), every level read by k_fast (detection), the records
     written by k_orient_desc.  Nothing else counts (padding, intermediates, re-reads)."""
     lv = level_sizes(W, H)
     px = [w * h for w, h in lv]
     return {
         "k_pyr0": B * px[0],
         "k_pyr_resize": B * sum(px[1:]) / (len(lv) - 1),
-        "k_level": B * sum(px),
+        "k_fast": B * sum(px),
         "k_select": 0,
         "k_orient_desc": 60 * n_kp,
     }
@@ -295,7 +295,9 @@ def latency_b1(orb, W, H, NF, device, frames, reps=100):
         "cpu_oracle_single_thread_extract_ms": c_ext * 1e3,
         "cpu_oracle_single_thread_sfi_ms": c_sfi * 1e3,
         "note": f"{W}x{H}, {NF} kp, {reps} calls each through the Python binding (ctypes); host entries include "
-                "H2D/D2H and a stream synchronisation per call",
+                "the H2D/D2H copies through the handle's pinned staging and one stream synchronisation per call; "
+                "batches below 32 / 256 frames run the FAST(7) re-runs / the small pyramid levels with "
+                "per-level multi-workgroup launches (k_rerun, k_pyr_resize)",
     }
 
 

@@ -256,19 +256,20 @@ __device__ __forceinline__ void stage_tile16(uint4* __restrict__ dst, const uint
 // before any LDS write, so a tile costs one memory round trip instead of one per row group
 // (k_level's wide tiles).
 #define SB 20
+template <int NT>
 __device__ __forceinline__ void stage_rows_to_lds(uint32_t* __restrict__ dst, int lsw,
                                                   const uint32_t* __restrict__ src, long long gsw, int rows,
                                                   int words, int wlimit, int tid) {
     const int total = rows * words;
-    const int dr = 256 / words, dc = 256 - dr * words;
-    for (int base = 0; base < total; base += SB * 256) {
+    const int dr = NT / words, dc = NT - dr * words;  // (words > NT: dr = 0, one carry)
+    for (int base = 0; base < total; base += SB * NT) {
         const int i0 = base + tid;
         const int r0 = i0 / words, c0 = i0 - r0 * words;
         uint32_t v[SB];
         int r = r0, c = c0;
 #pragma unroll
         for (int k = 0; k < SB; ++k) {
-            v[k] = (base + k * 256 + tid < total && c < wlimit) ? src[(long long)r * gsw + c] : 0u;
+            v[k] = (base + k * NT + tid < total && c < wlimit) ? src[(long long)r * gsw + c] : 0u;
             r += dr;
             c += dc;
             if (c >= words) {
@@ -280,7 +281,7 @@ __device__ __forceinline__ void stage_rows_to_lds(uint32_t* __restrict__ dst, in
         c = c0;
 #pragma unroll
         for (int k = 0; k < SB; ++k) {
-            if (base + k * 256 + tid < total) dst[r * lsw + c] = v[k];
+            if (base + k * NT + tid < total) dst[r * lsw + c] = v[k];
             r += dr;
             c += dc;
             if (c >= words) {
@@ -523,101 +524,10 @@ __global__ void __launch_bounds__(RT_THREADS) k_pyr_resize_tail(uint8_t* __restr
     }
 }
 
-// ---- FAST per cell ----------------------------------------------------------------------
-// One workgroup (4 waves) per (cell, frame); the cell ROI (cell + 3 px each side) is staged
-// in LDS.  For threshold t = fastTh (and again at t = 7 when that finds <= 3 corners,
-// ORBextractor.cc:609-614):
-//   detect  compass pre-filter (a 9-arc always covers two adjacent points of {0,4,8,12},
-//           the SSE2 pre-test of cv::FAST), full 16-point 9-arc test only in wave segments
-//           where some lane passed it; corners are queued in LDS
-//   score   exact S (cornerScore<16> + 1) for the queued corners only
-//   nms     3x3 non-max suppression around each queued corner; neighbours outside the
-//           detection region, and non-corners, score 0 — cv::FAST on a cell-sized Mat
-// then the survivors are compacted in raster order as (score << 24) | (y << 12) | x.
-
-typedef short i16x2_t __attribute__((ext_vector_type(2)));
-// cv::FAST corner test at threshold t: >= 9 contiguous circle pixels all > v+t or all < v-t.
-// Packed 16-bit arithmetic: circle points k and k + 8 share a dword; the sign bits of
-// (v + t) - c and c - (v - t) are the bright / dark flags (values within i16 for any t <= 255).
-// About 70 VALU instead of ~120 for 32 compare/select pairs: this test runs on every pixel
-// that passes the compass pre-filter (k_level is VALU-issue bound).
-__device__ __forceinline__ bool fast_is_corner(const uint8_t* p, int TP, int t) {
-    const int v = p[0];
-    const uint32_t d0 = p[3 * TP] | (uint32_t)p[-3 * TP] << 16;           // c0,  c8
-    const uint32_t d1 = p[3 * TP + 1] | (uint32_t)p[-3 * TP - 1] << 16;   // c1,  c9
-    const uint32_t d2 = p[2 * TP + 2] | (uint32_t)p[-2 * TP - 2] << 16;   // c2,  c10
-    const uint32_t d3 = p[TP + 3] | (uint32_t)p[-TP - 3] << 16;           // c3,  c11
-    const uint32_t d4 = p[3] | (uint32_t)p[-3] << 16;                     // c4,  c12
-    const uint32_t d5 = p[-TP + 3] | (uint32_t)p[TP - 3] << 16;           // c5,  c13
-    const uint32_t d6 = p[-2 * TP + 2] | (uint32_t)p[2 * TP - 2] << 16;   // c6,  c14
-    const uint32_t d7 = p[-3 * TP + 1] | (uint32_t)p[3 * TP - 1] << 16;   // c7,  c15
-    const uint32_t d[8] = {d0, d1, d2, d3, d4, d5, d6, d7};
-    const short hi = (short)(v + t), lo = (short)(v - t);
-    const i16x2_t H = {hi, hi}, L = {lo, lo};
-    uint32_t mb = 0, md = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const i16x2_t c = __builtin_bit_cast(i16x2_t, d[k]);
-        mb |= (__builtin_bit_cast(uint32_t, (i16x2_t)(H - c)) & 0x80008000u) >> k;
-        md |= (__builtin_bit_cast(uint32_t, (i16x2_t)(c - L)) & 0x80008000u) >> k;
-    }
-    // flag k at bit 15 - k, flag k + 8 at bit 31 - k: bits 0..15 of (mb >> 24) | (mb & 0xFF00)
-    // run through flags 15..0, the circle in reverse cyclic order
-    const uint32_t bri = (mb >> 24) | (mb & 0xFF00u), drk = (md >> 24) | (md & 0xFF00u);
-    auto has9 = [](uint32_t m) {
-        const uint32_t m32 = m | (m << 16);
-        const uint32_t a2 = m32 & (m32 >> 1);
-        const uint32_t a4 = a2 & (a2 >> 2);
-        const uint32_t a8 = a4 & (a4 >> 4);
-        return (a8 & (m32 >> 8) & 0xFFFFu) != 0;
-    };
-    return has9(bri) || has9(drk);
-}
-
-__device__ __forceinline__ int fast_exact_strength(const uint8_t* p, int TP) {
-    int c[16];
-    c[0] = p[3 * TP];
-    c[1] = p[3 * TP + 1];
-    c[2] = p[2 * TP + 2];
-    c[3] = p[TP + 3];
-    c[4] = p[3];
-    c[5] = p[-TP + 3];
-    c[6] = p[-2 * TP + 2];
-    c[7] = p[-3 * TP + 1];
-    c[8] = p[-3 * TP];
-    c[9] = p[-3 * TP - 1];
-    c[10] = p[-2 * TP - 2];
-    c[11] = p[-TP - 3];
-    c[12] = p[-3];
-    c[13] = p[TP - 3];
-    c[14] = p[2 * TP - 2];
-    c[15] = p[3 * TP - 1];
-    const int v = p[0];
-    // A = max over arcs of min(v - c), B = max over arcs of min(c - v): sliding minima by
-    // doubling on (v - c, c - v) pairs
-    int a[24], bq[24];
-#pragma unroll
-    for (int k = 0; k < 24; ++k) {
-        a[k] = min(v - c[k & 15], v - c[(k + 1) & 15]);
-        bq[k] = min(c[k & 15] - v, c[(k + 1) & 15] - v);
-    }
-#pragma unroll
-    for (int k = 0; k < 22; ++k) {
-        a[k] = min(a[k], a[k + 2]);
-        bq[k] = min(bq[k], bq[k + 2]);
-    }
-    int A = -1000, B = -1000;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const int ma = min(min(a[k], a[k + 4]), v - c[(k + 8) & 15]);
-        const int mb = min(min(bq[k], bq[k + 4]), c[(k + 8) & 15] - v);
-        A = max(A, ma);
-        B = max(B, mb);
-    }
-    return max(A, B);
-}
-
-// The same strength with both sides in one packed register: lane 0 of each i16x2 carries the
+// ---- FAST strength --------------------------------------------------------------------------
+// S(p) = 1 + cornerScore<16>(p) of cv::FAST: the largest t for which p is a corner is S - 1,
+// so p is a corner at threshold t <=> S > t; records carry S - 1 as the score.
+// Both sides in one packed register: lane 0 of each i16x2 carries the
 // dark contrast v - c, lane 1 the bright contrast c - v; arcs of 9 by doubling windows
 // (2, then 2+2+2+2+1), both sides per instruction.  ~130 VALU and 16 registers of
 // circle values: cheap enough to run on every pre-filter survivor instead of a 9-arc test
@@ -651,11 +561,16 @@ __device__ __forceinline__ int fast_strength_packed(const uint8_t* p, int TP) {
 }
 
 // The reference's `FAST(cellImage, keys, 7, true)` re-run of a cell that kept <= 3 corners at
-// fastTh (ORBextractor.cc:609-614), by the whole 256-thread workgroup: the cell ROI with its
+// fastTh (ORBextractor.cc:609-614), by a whole 256-thread workgroup: the cell ROI with its
 // 3 px ring is staged into LDS with dword loads, the strength plane at t = 7 computed, 3x3
 // strict NMS inside the detection region (out-of-region neighbours 0, as cv::FAST on the cell
 // Mat), survivors written in raster order as ((S - 1) << 24) | (y << 12) | x.  Returns the
-// survivor count (all threads).  smem: Sp (dwp x dh) | Fl (dwp x dh) | rowc | In.
+// survivor count (all threads).  smem: Sp (dwp x dh) | Fl (dwp x dh) | rowc | In, rerun_lds()
+// bytes.
+inline size_t rerun_lds(int dw, int dh) {
+    const size_t dwp = (size_t)((dw + 3) & ~3), inW = (size_t)((3 + dw + 6 + 3) & ~3);
+    return 2 * dwp * dh + 4 * (size_t)((dh + 3) & ~3) + inW * (dh + 6) + 16;
+}
 __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int dw, int dh, int rx0, int ry0, int t,
                                uint8_t* smem, uint32_t* __restrict__ out, int tid) {
     const int wave = tid >> 6, lane = tid & 63;
@@ -671,45 +586,14 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
         const int nwr = inW >> 2, pw = pitch >> 2;
         // all loads of a batch in flight before any LDS write (one round trip per 20 dwords
         // per thread, instead of one per row group)
-        stage_rows_to_lds((uint32_t*)In, nwr, src, pw, dh + 6, nwr, nwr, tid);
+        stage_rows_to_lds<256>((uint32_t*)In, nwr, src, pw, dh + 6, nwr, nwr, tid);
         for (int i = tid; i < nw; i += 256) ((uint32_t*)Fl)[i] = 0u;
     }
     __syncthreads();
-    // corner test per pixel; corners queued per wave and their exact strengths computed 64 at
-    // a time with every lane busy (textured cells have corners in most 64-pixel chunks)
-    {
-        uint32_t* rq = (uint32_t*)(In + (((size_t)inW * (dh + 6) + 3) & ~(size_t)3)) + wave * 128;
-        const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-        int pn = 0;
-        auto flush64 = [&]() {  // strengths of rq[0..63], then the rest moves to the front
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            const uint32_t q = rq[lane];
-            const int qy = (int)(q >> 16), qx = (int)(q & 0xFFFFu);
-            Sp[qy * dwp + qx] = (uint8_t)fast_exact_strength(In + (qy + 3) * inW + qx + 3 + o, inW);
-            const uint32_t r = 64 + lane < pn ? rq[64 + lane] : 0u;
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (64 + lane < pn) rq[lane] = r;
-            pn -= 64;
-        };
-        for (int yy = wave; yy < dh; yy += 4)
-            for (int xx0 = 0; xx0 < dw; xx0 += 64) {
-                const int xx = xx0 + lane;
-                bool corner = false;
-                if (xx < dw) {
-                    corner = fast_is_corner(In + (yy + 3) * inW + xx + 3 + o, inW, t);
-                    Sp[yy * dwp + xx] = 0;
-                }
-                const uint64_t m = __ballot(corner);
-                if (corner) rq[pn + __popcll(m & below)] = ((uint32_t)yy << 16) | (uint32_t)xx;
-                pn += __popcll(m);
-                if (pn >= 64) flush64();
-            }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane < pn) {
-            const uint32_t q = rq[lane];
-            const int qy = (int)(q >> 16), qx = (int)(q & 0xFFFFu);
-            Sp[qy * dwp + qx] = (uint8_t)fast_exact_strength(In + (qy + 3) * inW + qx + 3 + o, inW);
-        }
+    // the strength of every pixel (corner at t <=> S > t; the NMS below reads only S > t)
+    for (int i = tid; i < dh * dw; i += 256) {
+        const int yy = i / dw, xx = i - yy * dw;
+        Sp[yy * dwp + xx] = (uint8_t)max(fast_strength_packed(In + (yy + 3) * inW + xx + 3 + o, inW), 0);
     }
     __syncthreads();
     // 3x3 NMS; each row's survivor count comes from the same ballots (no second pass)
@@ -785,6 +669,56 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
     const int total = s_total;
     __syncthreads();  // smem is reused by the caller
     return total;
+}
+
+// The FAST(7) re-runs of every (frame, level) for small batches (the per-frame latency path),
+// before k_select<.., false>: NWG workgroups per (frame, level), workgroup (b * NWG + gw, l)
+// re-running the level's fallback cells gw, gw + NWG, ... (in cell order), so one frame's
+// re-runs — serial inside k_select's single workgroup per level — spread over many CUs.  A
+// cell re-runs where the reference's does: not skipped, and min(count, cap) <= 3 with 0 for a
+// cell with no detection area.  The new count is stored with RERUN_FLAG set, so a workgroup
+// deciding later still counts the cell among the fallback cells (the ordinal -> workgroup
+// assignment is the same everywhere, and so is the decision of every wave of a workgroup).
+// Large batches keep the re-runs inside k_select<.., true>: there every CU is busy anyway.
+#define RERUN_FLAG 0x40000000
+#define COUNT_MASK 0x3FFFFFFF
+__global__ void __launch_bounds__(256) k_rerun(const uint8_t* __restrict__ pyr, uint32_t* __restrict__ cand,
+                                               int* __restrict__ cellCount, Geom g,
+                                               const CellGeom* __restrict__ cells, int NWG) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int b = blockIdx.x / NWG, gw = blockIdx.x - b * NWG, l = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const LevelGeom& lg = g.lv[l];
+    const int nC = lg.rows * lg.cols;
+    const CellGeom* lc = cells + lg.cell0;
+    uint32_t* fcand = cand + (long long)b * g.candPerFrame;
+    int* fcount = cellCount + (long long)b * g.nCells + lg.cell0;
+    int ord = 0;
+    for (int c0 = 0; c0 < nC; c0 += 64) {
+        const int c = c0 + lane;
+        bool fb = false;
+        if (c < nC) {
+            const CellGeom& cg = lc[c];
+            const int cnt = fcount[c];
+            const int n = (cg.hx <= 6 || cg.hy <= 6) ? 0 : min(cnt & COUNT_MASK, cg.cap);
+            fb = (cnt & RERUN_FLAG) || (!cg.skipped && n <= 3);
+        }
+        uint64_t m = __ballot(fb);
+        while (m) {
+            const int cc = c0 + __builtin_ctzll(m);
+            m &= m - 1;
+            if (ord++ % NWG != gw) continue;
+            const CellGeom cg = lc[cc];
+            const int dw = cg.hx - 6, dh = cg.hy - 6;
+            int n = 0;
+            if (dw > 0 && dh > 0) {
+                const uint8_t* det = pyr + lg.base + (long long)b * lg.fstride +
+                                     (long long)(EDGE + cg.y0 + 3) * lg.pitch + EDGE + cg.x0 + 3;
+                n = cell_fast_rerun(det, lg.pitch, dw, dh, cg.x0 + 3, cg.y0 + 3, 7, smem, fcand + cg.candOff, tid);
+            }
+            if (tid == 0) fcount[cc] = n | RERUN_FLAG;
+        }
+    }
 }
 
 // ---- selection (retainBest replay) -------------------------------------------------------
@@ -867,10 +801,16 @@ __device__ __forceinline__ int cell_of(const int* off, int n, int i) {
     return lo;
 }
 
+#ifndef KR_TAIL_BATCH
+#define KR_TAIL_BATCH 256  // batches below this resize every level with its own launch
+#endif
+#ifndef KS_SEP_BATCH
+#define KS_SEP_BATCH 32  // batches below this re-run FAST(7) cells in k_rerun, not in k_select
+#endif
 #ifndef KS_WAVES
 #define KS_WAVES 2  // waves per SIMD the register allocation targets
 #endif
-template <bool HARRIS>
+template <bool HARRIS, bool RERUN>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAVES))) k_select(const uint8_t* __restrict__ pyr, uint32_t* __restrict__ cand,
                                                 uint32_t* __restrict__ cand2, int* __restrict__ cellCount, Geom g,
                                                 const CellGeom* __restrict__ cells, uint32_t* __restrict__ lvlOut,
@@ -893,7 +833,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
     const CellGeom* lc = cells + lg.cell0;
     uint32_t* fcand = cand + (long long)b * g.candPerFrame;
     int* fcount = cellCount + (long long)b * g.nCells + lg.cell0;
-    if (wave == 0) {  // counts, skip flags, and the list of cells to re-run (ascending)
+    if (wave == 0) {  // counts, skip flags, and the list of cells to re-run (ascending, RERUN)
         constexpr int CPL = ORB_MAX_CELLS_PER_LEVEL / 64;
         int cnt[CPL], cap[CPL], skip[CPL], hx[CPL], hy[CPL], coff[CPL];
 #pragma unroll
@@ -914,11 +854,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
             const int c = 64 * j + lane;
             bool fb = false;
             if (c < nC) {
-                const int n = (skip[j] || hx[j] <= 6 || hy[j] <= 6) ? 0 : min(cnt[j], cap[j]);
+                // (k_rerun's counts carry RERUN_FLAG; such a cell has been re-run: not again)
+                const int n = (skip[j] || hx[j] <= 6 || hy[j] <= 6) ? 0 : min(cnt[j] & COUNT_MASK, cap[j]);
                 s_cnt[c] = n;
                 s_skip[c] = (uint8_t)skip[j];
                 s_coff[c] = coff[j];
-                fb = !skip[j] && n <= 3;
+                fb = RERUN && !skip[j] && n <= 3;
             }
             const uint64_t m = __ballot(fb);
             if (fb) s_fb[nfb + __popcll(m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))))] = c;
@@ -930,7 +871,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
     // (1) FAST(cellImage, keys, 7, true) where a cell kept <= 3 (a skipped cell is `continue`d)
     {
         const int nfb = s_fb[ORB_MAX_CELLS_PER_LEVEL];
-        for (int f = 0; f < (KS_SKIP_RERUN ? 0 : nfb); ++f) {
+        for (int f = 0; f < (RERUN && !KS_SKIP_RERUN ? nfb : 0); ++f) {
             const int c = s_fb[f];
             const CellGeom cg = lc[c];
             const int dw = cg.hx - 6, dh = cg.hy - 6;
@@ -2193,7 +2134,7 @@ struct orb_extractor {
     Geom g{};
     std::vector<CellGeom> cells;
     std::vector<int> rtab;
-    size_t cellLds = 0, selectLds = 0;
+    size_t cellLds = 0, selectLds = 0;  // a FAST(7) re-run's LDS (largest cell); k_select's
     size_t resizeLds[ORB_MAX_LEVELS] = {};
     int resizeTail = 0;           // first level of k_pyr_resize_tail (nlevels: none)
     int tailBufA = 0, tailBufB = 0;
@@ -2229,9 +2170,18 @@ struct orb_extractor {
     uint8_t* d_img = nullptr;
     uint8_t* d_imgColor = nullptr;  // orb_extract_color's interleaved frame
     size_t imgColorCap = 0;
+    // one device block: counts (maxBatch, padded to 256 B) | keypoints | descriptors, so a
+    // single-frame download of the count and frame 0's keypoints is one contiguous copy
+    uint8_t* d_out = nullptr;
     orb_keypoint_t* d_kps = nullptr;
     uint8_t* d_desc = nullptr;
     int* d_counts = nullptr;
+    size_t countsPad = 0;
+    // pinned host staging of the single-frame host entry points (orb_extract, orb_extract_color):
+    // frame (W x H x up to 4 channels) | count + keypoints | descriptors, mirroring d_out, so the
+    // uploads and downloads are DMA from page-locked memory and nothing is allocated per call
+    uint8_t* h_pin = nullptr;
+    size_t pinImg = 0;
 
     void free_events() {
         for (auto e : evPool) hipEventDestroy(e);
@@ -2254,9 +2204,8 @@ struct orb_extractor {
         hipFree(d_cells);
         hipFree(d_img);
         hipFree(d_imgColor);
-        hipFree(d_kps);
-        hipFree(d_desc);
-        hipFree(d_counts);
+        hipFree(d_out);
+        if (h_pin) (void)hipHostFree(h_pin);
         d_pyr = nullptr;
         d_tiles = nullptr;
         nTiles = 0;
@@ -2272,9 +2221,12 @@ struct orb_extractor {
         d_img = nullptr;
         d_imgColor = nullptr;
         imgColorCap = 0;
+        d_out = nullptr;
         d_kps = nullptr;
         d_desc = nullptr;
         d_counts = nullptr;
+        h_pin = nullptr;
+        pinImg = 0;
         W = H = 0;
         pyrBatch = 0;
     }
@@ -2323,6 +2275,7 @@ struct orb_extractor {
         G.umaxNib = 0;
         for (int v = 0; v < 16; ++v) G.umaxNib |= (unsigned long long)umax[v] << (4 * v);
         std::vector<CellGeom> cl;
+        cellLds = 0;
         std::vector<int> rt;
         long long pyrBytes = 0;
         int cand = 0, kpBase = 0;
@@ -2415,11 +2368,7 @@ struct orb_extractor {
                                 return set_err(ORB_ENOTSUP, "cell ROI outside the level (the reference asserts)");
                             int dw = c.hx - 6, dh = c.hy - 6;
                             c.cap = (dw > 0 && dh > 0) ? ((dw + 1) / 2) * ((dh + 1) / 2) : 0;
-                            const size_t dwp = (size_t)((std::max(dw, 0) + 3) & ~3);
-                            const size_t inW = (size_t)((3 + std::max(dw, 0) + 6 + 3) & ~3);
-                            size_t lds = 2 * dwp * std::max(dh, 0) + 4 * (size_t)((std::max(dh, 0) + 3) & ~3) +
-                                         inW * (std::max(dh, 0) + 6) + 16 + 4 * 4 * 128;  // + corner queues
-                            cellLds = std::max(cellLds, lds);
+                            if (dw > 0 && dh > 0) cellLds = std::max(cellLds, rerun_lds(dw, dh));
                         }
                     }
                     cl.push_back(c);
@@ -2571,9 +2520,58 @@ struct orb_extractor {
     int ensure_staging() {
         if (d_img) return ORB_OK;
         HIP_TRY(hipMalloc(&d_img, (size_t)W * H * maxBatch));
-        HIP_TRY(hipMalloc(&d_kps, (size_t)std::max(kpCap, 1) * maxBatch * sizeof(orb_keypoint_t)));
-        HIP_TRY(hipMalloc(&d_desc, (size_t)std::max(kpCap, 1) * maxBatch * 32));
-        HIP_TRY(hipMalloc(&d_counts, (size_t)maxBatch * 4));
+        const size_t cap = (size_t)std::max(kpCap, 1);
+        countsPad = ((size_t)maxBatch * 4 + 255) & ~(size_t)255;
+        const size_t kpsBytes = ((cap * maxBatch * sizeof(orb_keypoint_t)) + 255) & ~(size_t)255;
+        HIP_TRY(hipMalloc(&d_out, countsPad + kpsBytes + cap * maxBatch * 32));
+        d_counts = (int*)d_out;
+        d_kps = (orb_keypoint_t*)(d_out + countsPad);
+        d_desc = d_out + countsPad + kpsBytes;
+        return ORB_OK;
+    }
+
+    // single-frame pinned staging: [frame: pinImg][count + frame-0 keypoints: countsPad + kpCap*28][descriptors]
+    int ensure_pinned(size_t frameBytes) {
+        if (h_pin && frameBytes <= pinImg) return ORB_OK;
+        if (h_pin) {
+            HIP_TRY(hipStreamSynchronize(stream));  // the previous call's copies are complete anyway
+            (void)hipHostFree(h_pin);
+            h_pin = nullptr;
+            pinImg = 0;
+        }
+        const size_t img = (std::max(frameBytes, (size_t)W * H * 4) + 255) & ~(size_t)255;
+        const size_t cap = (size_t)std::max(kpCap, 1);
+        HIP_TRY(hipHostMalloc((void**)&h_pin, img + countsPad + cap * (sizeof(orb_keypoint_t) + 32), 0));
+        pinImg = img;
+        return ORB_OK;
+    }
+
+    // host frame (rows at `stride`) -> pinned -> device at `dst` (tight rows of `row` bytes)
+    int upload_frame(uint8_t* dst, const uint8_t* img, size_t row, int hgt, size_t stride) {
+        if (int r = ensure_pinned(row * hgt)) return r;
+        if (stride == row) {
+            std::memcpy(h_pin, img, row * hgt);
+        } else {
+            for (int y = 0; y < hgt; ++y) std::memcpy(h_pin + row * y, img + stride * y, row);
+        }
+        HIP_TRY(hipMemcpyAsync(dst, h_pin, row * hgt, hipMemcpyHostToDevice, stream));
+        return ORB_OK;
+    }
+
+    // frame 0's count, keypoints and descriptors -> the caller's buffers (one stream sync)
+    int download_frame0(orb_keypoint_t* kps_out, int kps_cap, uint8_t* desc_out, int* n_out) {
+        const size_t cap = (size_t)std::max(kpCap, 1);
+        uint8_t* pk = h_pin + pinImg;
+        uint8_t* pd = pk + countsPad + cap * sizeof(orb_keypoint_t);
+        HIP_TRY(hipMemcpyAsync(pk, d_out, countsPad + cap * sizeof(orb_keypoint_t), hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipMemcpyAsync(pd, d_desc, cap * 32, hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+        int n = 0;
+        std::memcpy(&n, pk, 4);
+        if (n > kps_cap) return set_err(ORB_ERANGE, "kps_cap smaller than the number of keypoints");
+        std::memcpy(kps_out, pk + countsPad, (size_t)n * sizeof(orb_keypoint_t));
+        std::memcpy(desc_out, pd, (size_t)n * 32);
+        *n_out = n;
         return ORB_OK;
     }
 
@@ -2659,12 +2657,15 @@ struct orb_extractor {
         }
         stage_end(0, st);
         stage_begin(1, st);
-        for (int l = 1; l < resizeTail; ++l) {
+        // a few frames: one multi-workgroup launch per level (the tail kernel's one workgroup
+        // per frame walks its levels serially, the latency floor of a single frame)
+        const int tail = B < KR_TAIL_BATCH ? nlevels : resizeTail;
+        for (int l = 1; l < tail; ++l) {
             const LevelGeom& lg = g.lv[l];
             dim3 grid((lg.pitch + RZ_TW - 1) / RZ_TW, (lg.ph + RZ_TH - 1) / RZ_TH, B);
             hipLaunchKernelGGL(k_pyr_resize, grid, dim3(256), resizeLds[l], st, d_pyr, d_rtab, g.lv[l], g.lv[l - 1]);
         }
-        if (resizeTail < nlevels)
+        if (tail < nlevels)
             hipLaunchKernelGGL(k_pyr_resize_tail, dim3(B), dim3(RT_THREADS), tailLds, st, d_pyr, d_rtab, g, resizeTail,
                                tailBufA, tailBufB);
         stage_end(1, st);
@@ -2679,12 +2680,30 @@ struct orb_extractor {
         hipLaunchKernelGGL(k_fast, dim3(nTiles, B), dim3(256), 0, st, d_pyr, g, d_tiles, d_cand, d_cellCount);
         stage_end(2, st);
         stage_begin(3, st);
-        if (scoreType == ORB_HARRIS_SCORE)
-            hipLaunchKernelGGL(k_select<true>, dim3(B, nlevels), dim3(256), selectLds, st, d_pyr, d_cand, d_cand2,
-                               d_cellCount, g, d_cells, d_lvl, d_lvlCount, d_candH, d_lvlResp, harrisScale4);
-        else
-            hipLaunchKernelGGL(k_select<false>, dim3(B, nlevels), dim3(256), selectLds, st, d_pyr, d_cand, d_cand2,
-                               d_cellCount, g, d_cells, d_lvl, d_lvlCount, (uint64_t*)nullptr, (float*)nullptr, 0.f);
+        // FAST(7) re-runs: inside k_select (one workgroup per level and frame) when the batch
+        // fills the chip; for a few frames spread over NWG workgroups per level first (k_rerun)
+        const bool sep = B < KS_SEP_BATCH && cellLds;
+        if (sep && !KS_SKIP_RERUN) {
+            const int NWG = std::min(32, std::max(1, 512 / (B * nlevels)));
+            hipLaunchKernelGGL(k_rerun, dim3(B * NWG, nlevels), dim3(256), cellLds, st, d_pyr, d_cand, d_cellCount, g,
+                               d_cells, NWG);
+        }
+        const dim3 sg(B, nlevels);
+        if (scoreType == ORB_HARRIS_SCORE) {
+            if (sep)
+                hipLaunchKernelGGL((k_select<true, false>), sg, dim3(256), selectLds, st, d_pyr, d_cand, d_cand2,
+                                   d_cellCount, g, d_cells, d_lvl, d_lvlCount, d_candH, d_lvlResp, harrisScale4);
+            else
+                hipLaunchKernelGGL((k_select<true, true>), sg, dim3(256), selectLds, st, d_pyr, d_cand, d_cand2,
+                                   d_cellCount, g, d_cells, d_lvl, d_lvlCount, d_candH, d_lvlResp, harrisScale4);
+        } else {
+            if (sep)
+                hipLaunchKernelGGL((k_select<false, false>), sg, dim3(256), selectLds, st, d_pyr, d_cand, d_cand2,
+                                   d_cellCount, g, d_cells, d_lvl, d_lvlCount, (uint64_t*)nullptr, (float*)nullptr, 0.f);
+            else
+                hipLaunchKernelGGL((k_select<false, true>), sg, dim3(256), selectLds, st, d_pyr, d_cand, d_cand2,
+                                   d_cellCount, g, d_cells, d_lvl, d_lvlCount, (uint64_t*)nullptr, (float*)nullptr, 0.f);
+        }
         stage_end(3, st);
         stage_begin(4, st);
         dim3 gd((std::max(kpCap, 1) + 3) / 4, B);
@@ -2753,7 +2772,11 @@ int orb_extractor_create(int nfeatures, float scale_factor, int nlevels, int sco
     int st = upload_pattern(device);
     if (st) return st;
     // k_select<true> (HARRIS_SCORE) stages (response, record) pairs: up to 96 KB of LDS
-    hipFuncSetAttribute((const void*)k_select<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    hipFuncSetAttribute((const void*)k_select<true, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    hipFuncSetAttribute((const void*)k_select<true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    hipFuncSetAttribute((const void*)k_select<false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    hipFuncSetAttribute((const void*)k_select<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    hipFuncSetAttribute((const void*)k_rerun, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
     hipFuncSetAttribute((const void*)k_pyr_resize_tail, hipFuncAttributeMaxDynamicSharedMemorySize, RT_LDS_MAX);
     orb_extractor* h = new orb_extractor();
     h->nfeatures = nfeatures;
@@ -2841,10 +2864,13 @@ int orb_extract_batch(orb_extractor_t* h, int B, const uint8_t* imgs, int w, int
     if (int r = h->order_after_last(h->stream)) return r;
     int st = h->ensure_staging();
     if (st) return st;
-    HIP_TRY(hipMemcpy2DAsync(h->d_img, w, imgs, stride, w, (size_t)hgt, hipMemcpyHostToDevice, h->stream));
-    for (int k = 1; k < B; ++k)
-        HIP_TRY(hipMemcpy2DAsync(h->d_img + (size_t)k * w * hgt, w, imgs + (size_t)k * frame_pitch, stride, w,
-                                 (size_t)hgt, hipMemcpyHostToDevice, h->stream));
+    if (stride == w && frame_pitch == (int64_t)w * hgt) {  // tight frames: one linear copy
+        HIP_TRY(hipMemcpyAsync(h->d_img, imgs, (size_t)B * w * hgt, hipMemcpyHostToDevice, h->stream));
+    } else {
+        for (int k = 0; k < B; ++k)
+            HIP_TRY(hipMemcpy2DAsync(h->d_img + (size_t)k * w * hgt, w, imgs + (size_t)k * frame_pitch, stride, w,
+                                     (size_t)hgt, hipMemcpyHostToDevice, h->stream));
+    }
     st = h->launch(B, h->d_img, w, (long long)w * hgt, h->d_kps, h->d_desc, h->d_counts, h->stream);
     if (st) return st;
     HIP_TRY(hipMemcpyAsync(n_out, h->d_counts, (size_t)B * 4, hipMemcpyDeviceToHost, h->stream));
@@ -2863,16 +2889,21 @@ int orb_extract(orb_extractor_t* h, const uint8_t* img, int w, int hgt, int stri
         return ORB_OK;
     }
     if (!img || !kps_out || !desc_out) return set_err(ORB_EINVAL, "bad arguments");
-    std::vector<orb_keypoint_t> k(std::max(h->kpCap, 1));
-    std::vector<uint8_t> d((size_t)std::max(h->kpCap, 1) * 32);
-    int32_t n = 0;
-    int st = orb_extract_batch(h, 1, img, w, hgt, stride, (int64_t)stride * hgt, k.data(), d.data(), &n);
-    if (st) return st;
-    if (n > kps_cap) return set_err(ORB_ERANGE, "kps_cap smaller than the number of keypoints");
-    std::memcpy(kps_out, k.data(), (size_t)n * sizeof(orb_keypoint_t));
-    std::memcpy(desc_out, d.data(), (size_t)n * 32);
-    *n_out = n;
-    return ORB_OK;
+    if (stride < w) return set_err(ORB_EINVAL, "bad image geometry");
+    HIP_TRY(hipSetDevice(h->device));
+    if (w != h->W || hgt != h->H) {
+        if (int r = h->drain()) return r;
+        if (int r = h->build_geometry(w, hgt)) return r;
+    }
+    // the upload overwrites the staging a launch on another stream may still read
+    if (int r = h->order_after_last(h->stream)) return r;
+    if (int r = h->ensure_staging()) return r;
+    if (int r = h->upload_frame(h->d_img, img, (size_t)w, hgt, (size_t)stride)) return r;
+    if (int r = h->launch(1, h->d_img, w, (long long)w * hgt, h->d_kps, h->d_desc, h->d_counts, h->stream)) {
+        (void)hipStreamSynchronize(h->stream);
+        return r;
+    }
+    return h->download_frame0(kps_out, kps_cap, desc_out, n_out);
 }
 
 int orb_extract_batch_device_color(orb_extractor_t* h, int B, const uint8_t* d_imgs, int w, int hgt, int stride,
@@ -2921,22 +2952,14 @@ int orb_extract_color(orb_extractor_t* h, const uint8_t* img, int w, int hgt, in
         HIP_TRY(hipMalloc(&h->d_imgColor, row * hgt));
         h->imgColorCap = row * hgt;
     }
-    HIP_TRY(hipMemcpy2DAsync(h->d_imgColor, row, img, stride, row, (size_t)hgt, hipMemcpyHostToDevice, h->stream));
-    int32_t n = 0;
+    if (int r = h->upload_frame(h->d_imgColor, img, row, hgt, (size_t)stride)) return r;
     st = h->launch(1, h->d_imgColor, (int)row, (long long)(row * hgt), h->d_kps, h->d_desc, h->d_counts, h->stream,
                    channels, rgb);
     if (st) {
         (void)hipStreamSynchronize(h->stream);
         return st;
     }
-    HIP_TRY(hipMemcpyAsync(&n, h->d_counts, 4, hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(hipStreamSynchronize(h->stream));
-    if (n > kps_cap) return set_err(ORB_ERANGE, "kps_cap smaller than the number of keypoints");
-    HIP_TRY(hipMemcpyAsync(kps_out, h->d_kps, (size_t)n * sizeof(orb_keypoint_t), hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(hipMemcpyAsync(desc_out, h->d_desc, (size_t)n * 32, hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(hipStreamSynchronize(h->stream));
-    *n_out = n;
-    return ORB_OK;
+    return h->download_frame0(kps_out, kps_cap, desc_out, n_out);
 }
 
 int orb_descriptor_distance(const uint8_t* a, const uint8_t* b) {

@@ -8,7 +8,8 @@ FETCH_SIZE / WRITE_SIZE are in KiB per dispatch (TCC_EA0 request counters, MI355
 §HBM).  The guide's ×2 FETCH correction holds for 16-B/lane streaming loads; it is measured in
 the same run on k_pyr0, which reads exactly the B input frames (B·W·H bytes, evicted from the
 256 MiB Infinity Cache by the ~0.6 GB every step writes) with 16-B loads, and applied to the
-16-B-load kernels (k_pyr0, k_pyr_resize).  The dword-load kernels use the factor measured the
+16-B-load kernels (k_pyr0, k_pyr_resize, k_fast's tile staging, k_orient_desc's patch
+windows).  The dword-load kernels use the factor measured the
 same way when k_pyr0 still loaded dwords (r01_v16: 1.353).  WRITE_SIZE is taken as is (exact
 for streaming stores per the guide).
 """
@@ -19,7 +20,7 @@ import json
 from collections import defaultdict
 
 
-WIDE_LOADS = {"k_pyr0", "k_pyr_resize"}
+WIDE_LOADS = {"k_pyr0", "k_pyr_resize", "k_fast", "k_orient_desc"}
 
 
 def main():
@@ -52,8 +53,8 @@ def main():
     for k, d in sorted(mean.items()):
         if "FETCH_SIZE" not in d or "WRITE_SIZE" not in d:
             continue
-        # k_pyr0 / k_pyr_resize load 16 B per lane (calibrated here on k_pyr0's known read, the
-        # guide's x2); the other kernels load dwords (the r01_v16 dword calibration)
+        # WIDE_LOADS load 16 B per lane (calibrated here on k_pyr0's known read, the guide's x2);
+        # the other kernels load dwords (the r01_v16 dword calibration)
         rd = d["FETCH_SIZE"] * 1024.0 * ((cal or 1.0) if k in WIDE_LOADS else a.dword_factor)
         wr = d["WRITE_SIZE"] * 1024.0
         out["per_launch"][k] = {"fetch_kib": d["FETCH_SIZE"], "write_kib": d["WRITE_SIZE"], "read_bytes": rd,
