@@ -442,9 +442,9 @@ int orb_debug_level_image(orb_extractor_t* h, int b, int l, uint8_t* out, int* w
  * cell grid lets keypoints sit past the FAST border) (device sync). */
 int orb_debug_blur_image(orb_extractor_t* h, int b, int l, uint8_t* out);
 /* Per-cell FAST keypoint counts of frame b, level l (device sync); returns #cells. */
-/* k_level FAST-queue statistics of a -DKL_COUNT=1 timing build (zeros otherwise):
- * {lane-rows queued, pixels expanded, corners} summed since the last call (then cleared). */
-int orb_debug_klevel_counts(unsigned long long* out3); /* retired: zeros */
+/* Retired FAST-queue statistics hook of round 1's k_level (kept for ABI stability): writes
+ * three zeros. */
+int orb_debug_klevel_counts(unsigned long long* out3);
 int orb_debug_cell_counts(orb_extractor_t* h, int b, int l, int* counts, int cap);
 
 #ifdef __cplusplus

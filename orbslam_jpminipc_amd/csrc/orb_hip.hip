@@ -3,12 +3,13 @@
 // Pipeline for a batch of B same-size frames (all device-resident, one HIP stream):
 //   k_pyr0        level 0 + reflect-101 padding          (ORBextractor.cc:814-815)
 //   k_pyr_resize  level l from level l-1, fused padding   (ORBextractor.cc:800-807), l = 1..L-1
-//   k_level       per level tile: descriptor image (7x7 blur of the ROI, ORBextractor.cc:760)
-//                 and FAST at fastTh with the per-cell 3x3 NMS; survivors appended to their
-//                 cell's slots                              (ORBextractor.cc:560-607)
-//   k_select      per (frame, level): FAST(7) re-run of cells with <= 3 survivors (609-614),
-//                 raster order per cell, quota redistribution, retainBest per cell and per
-//                 level — exact libstdc++ nth_element replay (ORBextractor.cc:622-701)
+//                 (k_pyr_resize_tail: the small levels of a large batch in one launch)
+//   k_fast        per level tile: FAST strength at fastTh and the per-cell 3x3 NMS; survivors
+//                 appended to their cell's slots          (ORBextractor.cc:560-607)
+//   k_rerun       FAST(7) re-run of cells with <= 3 survivors (609-614), spread over many
+//                 workgroups (few or large frames; otherwise inside k_select)
+//   k_select      per (frame, level): raster order per cell, quota redistribution, retainBest
+//                 per cell and per level — exact libstdc++ nth_element replay (622-701)
 //   k_orient_desc per keypoint (one wave): IC angle on the raw level, rBRIEF on the
 //                 7x7 sigma-2 blur evaluated at the sample points, keypoint record
 //                                                          (ORBextractor.cc:124-194, 705-777)
@@ -42,9 +43,6 @@
 #endif
 #ifndef KL_SKIP_QUEUE
 #define KL_SKIP_QUEUE 0
-#endif
-#ifndef KF_TWO_PASS  // 1: queue = 9-arc test, compaction, then the strength of the corners
-#define KF_TWO_PASS 0
 #endif
 #ifndef KF_TIMING  // 1: per-phase s_memtime sums of k_fast's waves (experiment builds only)
 #define KF_TIMING 0
@@ -253,8 +251,7 @@ __device__ __forceinline__ void stage_tile16(uint4* __restrict__ dst, const uint
 
 // Stage `rows` x `words` dwords (global row pitch gsw dwords, columns >= wlimit read as 0)
 // into LDS (row pitch lsw dwords).  The block issues all its loads of a batch (SB per thread)
-// before any LDS write, so a tile costs one memory round trip instead of one per row group
-// (k_level's wide tiles).
+// before any LDS write, so a tile costs one memory round trip instead of one per row group.
 #define SB 20
 template <int NT>
 __device__ __forceinline__ void stage_rows_to_lds(uint32_t* __restrict__ dst, int lsw,
@@ -726,8 +723,9 @@ struct ScoreGreater {  // KeypointResponseGreater on the packed FAST score
     ORB_HD bool operator()(uint32_t a, uint32_t b) const { return (a >> 24) > (b >> 24); }
 };
 
-// One workgroup per (level, frame).  In: each cell's NMS survivors at fastTh from k_level, in
-// arrival order, and their count.  (1) cells with <= 3 survivors are re-run at t = 7; (2) each
+// One workgroup per (level, frame).  In: each cell's NMS survivors at fastTh from k_fast, in
+// arrival order, and their count.  (1) cells with <= 3 survivors are re-run at t = 7 (RERUN;
+// otherwise k_rerun did it); (2) each
 // cell's survivors are put in raster order — the order cv::FAST returns them, which
 // retainBest's nth_element depends on; (3) nToRetain / redistribution (ORBextractor.cc:622-670);
 // (4) retainBest per cell, concatenation in cell order, retainBest to the level quota
