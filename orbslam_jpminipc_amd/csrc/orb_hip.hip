@@ -2976,6 +2976,12 @@ int orb_descriptor_distance(const uint8_t* a, const uint8_t* b) {
     return dist;
 }
 
+#ifndef MATCH_NMAX_NUM
+#define MATCH_NMAX_NUM 9  // k_match_init's octave-0 capacity: NUM / 40 of the keypoint capacity
+#endif
+#ifndef MATCH_NMAX_MIN
+#define MATCH_NMAX_MIN 256
+#endif
 static size_t match_lds_bytes(int cap, int nmax) {
     // F2 slots (desc 32 + state 8 + x,y,a,cell 16) + queries (q2i,qx,qy 12 + top-8 32 + cnt 4)
     // + cap x (m12 4 + slot/bin 2)
@@ -2994,7 +3000,13 @@ int orb_search_for_initialization_batch_device(const orb_keypoint_t* d_kps, cons
     if (P == 0) return ORB_OK;
     if (bounds.max_x <= bounds.min_x || bounds.max_y <= bounds.min_y) return set_err(ORB_EINVAL, "bad bounds");
     if (cap > MATCH_BIG_NMAX) return set_err(ORB_ENOTSUP, "more than 8192 keypoints per frame");
-    const int nmax = std::min(cap, 1024);  // octave-0 keypoints per frame held in LDS by k_match_init
+    // octave-0 keypoints per frame held in LDS by k_match_init.  The extractor keeps at most
+    // mnFeaturesPerLevel[0] of them (0.217 nFeatures at scale 1.2, 8 levels), so 0.225 of the
+    // capacity covers its output and leaves room for two or more work-groups per CU (640x480:
+    // 0.233 -> 0.129 ms for 511 pairs, 1241x376: 0.47 -> 0.26); any frame beyond (another
+    // producer, another scale factor) is redone exactly by k_match_init_big below.
+    const int nmax =
+        std::min({cap, 1024, std::max(MATCH_NMAX_MIN, (int)(((long long)cap * MATCH_NMAX_NUM / 40 + 31) & ~31))});
     const size_t lds = match_lds_bytes(cap, nmax);
     const int nmaxBig = std::min(cap, MATCH_BIG_NMAX);
     const size_t ldsBig = match_big_lds_bytes(cap, nmaxBig);

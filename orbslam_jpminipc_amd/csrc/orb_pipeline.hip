@@ -5,12 +5,13 @@
 // ORBmatcher::SearchForInitialization between each frame and the next (Tracking::Initialize,
 // src/Tracking.cc:392-393) — the path bench.py measures.  Several kernels of the path are
 // latency-bound by construction (the nth_element replays of k_select, the greedy pass of
-// k_match_init), so the batch is cut into S contiguous chunks: chunk c is extracted by its own
-// extractor handle on its own stream and its internal pairs are matched there; the pair that
-// straddles chunks c-1 and c is matched on stream c after an event from chunk c-1's
-// extraction.  The chunks' kernels overlap on the device; results are those of the serial
-// path (same kernels, same inputs, disjoint outputs).  Events order the whole step after
-// earlier work on the caller's stream and before later work on it.
+// k_match_init), so the extraction is cut into S contiguous chunks, each extracted by its own
+// extractor handle on its own stream: the chunks' kernels overlap on the device (640x480,
+// B = 512, extraction alone: 2.30 ms on one stream, 2.18 on two).  All B-1 pairs are then
+// matched in one batch on the caller's stream after the chunks' events (matching on the chunk
+// streams, beside other chunks' extraction, was slower: 2.77 ms per step vs 2.58 serial).
+// Results are those of the serial path (same kernels, same inputs, disjoint outputs).  Events
+// order the whole step after earlier work on the caller's stream and before later work on it.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -37,7 +38,7 @@ struct orb_pipeline {
     int S = 0, device = 0, maxBatch = 0, cap = 0;
     std::vector<orb_extractor_t*> ext;
     std::vector<hipStream_t> streams;
-    std::vector<hipEvent_t> extracted, done;
+    std::vector<hipEvent_t> extracted;
     hipEvent_t start = nullptr;
     int32_t* d_iota = nullptr;  // 0 .. maxBatch: pair (b, b+1) = (iota[b], iota[b+1])
 
@@ -46,7 +47,6 @@ struct orb_pipeline {
         for (auto s : streams) (void)hipStreamSynchronize(s);
         for (auto e : ext) orb_extractor_destroy(e);
         for (auto e : extracted) (void)hipEventDestroy(e);
-        for (auto e : done) (void)hipEventDestroy(e);
         if (start) (void)hipEventDestroy(start);
         for (auto s : streams) (void)hipStreamDestroy(s);
         (void)hipFree(d_iota);
@@ -85,13 +85,11 @@ int orb_pipeline_create(int nfeatures, float scale_factor, int nlevels, int scor
     if (e != hipSuccess) return bail(e, "hipSetDevice");
     for (int c = 0; c < p->S; ++c) {
         hipStream_t s;
-        hipEvent_t a, b;
+        hipEvent_t a;
         if ((e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) != hipSuccess) return bail(e, "hipStreamCreate");
         p->streams.push_back(s);
         if ((e = hipEventCreateWithFlags(&a, hipEventDisableTiming)) != hipSuccess) return bail(e, "hipEventCreate");
         p->extracted.push_back(a);
-        if ((e = hipEventCreateWithFlags(&b, hipEventDisableTiming)) != hipSuccess) return bail(e, "hipEventCreate");
-        p->done.push_back(b);
     }
     if ((e = hipEventCreateWithFlags(&p->start, hipEventDisableTiming)) != hipSuccess) return bail(e, "hipEventCreate");
     std::vector<int32_t> iota(max_batch + 1);
@@ -134,26 +132,16 @@ int orb_pipeline_extract_and_match(orb_pipeline_t* p, int B, const uint8_t* d_im
                                           d_counts + b0, s);
         if (st) return st;
         PCHK(hipEventRecord(p->extracted[c], s));
-        // pairs (b, b + 1) inside the chunk; pair b's outputs at row b
-        if (n > 1) {
-            st = orb_search_for_initialization_batch_device(d_kps, d_desc, d_counts, cap, n - 1, p->d_iota + b0,
-                                                            p->d_iota + b0 + 1, bounds, nnratio, check_ori, window,
-                                                            nullptr, d_matches12 + (long long)b0 * cap,
-                                                            d_nmatches + b0, s);
-            if (st) return st;
-        }
-        // the pair straddling chunks c-1 and c
-        if (c > 0) {
-            PCHK(hipStreamWaitEvent(s, p->extracted[c - 1], 0));
-            st = orb_search_for_initialization_batch_device(d_kps, d_desc, d_counts, cap, 1, p->d_iota + b0 - 1,
-                                                            p->d_iota + b0, bounds, nnratio, check_ori, window,
-                                                            nullptr, d_matches12 + (long long)(b0 - 1) * cap,
-                                                            d_nmatches + b0 - 1, s);
-            if (st) return st;
-        }
-        PCHK(hipEventRecord(p->done[c], s));
     }
-    for (int c = 0; c < S; ++c) PCHK(hipStreamWaitEvent(caller, p->done[c], 0));
+    // every pair once the chunks are extracted, on the caller's stream: a matcher work-group
+    // takes most of a CU's LDS, so matching beside the extraction slowed both (measured)
+    for (int c = 0; c < S; ++c) PCHK(hipStreamWaitEvent(caller, p->extracted[c], 0));
+    if (B > 1) {
+        int st = orb_search_for_initialization_batch_device(d_kps, d_desc, d_counts, cap, B - 1, p->d_iota,
+                                                            p->d_iota + 1, bounds, nnratio, check_ori, window,
+                                                            nullptr, d_matches12, d_nmatches, caller);
+        if (st) return st;
+    }
     return ORB_OK;
 }
 

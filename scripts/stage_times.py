@@ -49,5 +49,19 @@ for _ in range(a.steps):
 torch.cuda.synchronize()
 prof = ext.profile_read()
 out = {n: round(ms / max(l, 1), 4) for n, (ms, l) in prof.items()}
+# SearchForInitialization on the B-1 consecutive pairs of the batch (the bench step's matcher)
+if B > 1:
+    m = orb.ORBmatcher(0.9, True)
+    f1 = torch.arange(B - 1, dtype=torch.int32, device="cuda")
+    f2 = f1 + 1
+    for _ in range(2):
+        m.search_for_initialization_batch_device(k, de, c, f1, f2, a.width, a.height, 100, stream=s)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(a.steps):
+        m.search_for_initialization_batch_device(k, de, c, f1, f2, a.width, a.height, 100, stream=s)
+    e1.record(s)
+    torch.cuda.synchronize()
+    out["k_match_init"] = round(e0.elapsed_time(e1) / a.steps, 4)
 out["lib"] = os.path.basename(str(_native.HIP_LIB_PATH))
 print(json.dumps(out))
