@@ -1425,6 +1425,7 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
 #define OD_WP 64   // LDS row pitch of the raw window (bytes)
 #define OD_HC 40   // row-pass columns: x-18 .. x+21 (10 groups of 4)
 #define OD_HPR 22  // row pairs of the row-pass sums (window rows 0 .. 43)
+#define OD_HOFF 128  // byte offset of the sums in the wave's buffer (see the row pass)
 #define GT_WA 0x37312212u  // bytes (x-3, x-2, x-1, x) -> 18, 34, 49, 55
 #define GT_WB 0x00122231u  // bytes (x+1, x+2, x+3, x+4) -> 49, 34, 18, 0
 // column-pass taps over row pairs (low half = the even row): rows r0-3 .. r0+4 when r0 is even
@@ -1480,8 +1481,8 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
                                                      const int* __restrict__ lvlCount, orb_keypoint_t* __restrict__ kps,
                                                      uint8_t* __restrict__ desc, int* __restrict__ counts,
                                                      const float* __restrict__ lvlResp) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_win[4][(2 * OD_WR + 1) * OD_WP];
-    __shared__ __attribute__((aligned(16))) uint32_t s_h[4][OD_HPR * OD_HC];
+    // per wave: the raw window, then (overlaid, OD_HOFF bytes in) the row-pass sums
+    __shared__ __attribute__((aligned(16))) uint8_t s_buf[4][OD_HOFF + OD_HPR * OD_HC * 4];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     // XCD-aware block order: workgroup i runs on XCD i % 8, so give each XCD a contiguous run
     // of keypoints (neighbouring keypoints share window rows: L2 hits instead of HBM re-reads)
@@ -1515,8 +1516,8 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
     const uint4* src = (const uint4*)(pyr + lg.base + (long long)b * lg.fstride +
                                       (long long)(y + EDGE - OD_WR) * lg.pitch + xa);
     const uint32_t pu = (uint32_t)lg.pitch >> 4;
-    uint8_t* W = s_win[wave];
-    uint32_t* Hs = s_h[wave];
+    uint8_t* W = s_buf[wave];
+    uint32_t* Hs = (uint32_t*)(s_buf[wave] + OD_HOFF);
     {
         constexpr int NU = (2 * OD_WR + 1) * 4;  // 172 16-byte units
         uint4 v[3];
@@ -1530,36 +1531,6 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
             if (lane + 64 * j < NU) ((uint4*)W)[lane + 64 * j] = v[j];
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS is in order per wave; compiler fence
-    // row pass: task = (4 window rows = 2 row pairs, group of 4 columns); window row r = level row
-    // y-21+r, sum column hc = level column x-18+hc; its 7 input bytes start at window byte
-    // x-5-xa+hc
-    {
-        const int o0 = x - 5 - xa;  // 0..15, wave-uniform
-        const int sb = o0 & 3, sd = o0 >> 2;
-        const uint32_t* W32 = (const uint32_t*)W;
-        for (int task = lane; task < (OD_HPR / 2) * (OD_HC / 4); task += 64) {
-            const int rq = task / (OD_HC / 4), gq = task - rq * (OD_HC / 4);
-            uint32_t h[4][4];
-#pragma unroll
-            for (int s2 = 0; s2 < 4; ++s2) {
-                const int r = min(4 * rq + s2, 2 * OD_WR);  // row 43 pads the last pair (tap 0)
-                // bytes 0 .. 9 of the span (byte 9 lies in d3 when sb == 3)
-                const uint32_t* q = W32 + r * (OD_WP / 4) + gq + sd;
-                const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3];
-                hrow4(__builtin_amdgcn_alignbyte(d1, d0, sb), __builtin_amdgcn_alignbyte(d2, d1, sb),
-                      __builtin_amdgcn_alignbyte(d3, d2, sb), h[s2]);
-            }
-#pragma unroll
-            for (int pr = 0; pr < 2; ++pr) {
-                uint4 o;
-                o.x = h[2 * pr][0] | (h[2 * pr + 1][0] << 16);
-                o.y = h[2 * pr][1] | (h[2 * pr + 1][1] << 16);
-                o.z = h[2 * pr][2] | (h[2 * pr + 1][2] << 16);
-                o.w = h[2 * pr][3] | (h[2 * pr + 1][3] << 16);
-                *(uint4*)(Hs + (2 * rq + pr) * OD_HC + 4 * gq) = o;
-            }
-        }
-    }
     // IC_Angle (ORBextractor.cc:124-151): the disc sums m10 = sum u*I, m01 = sum v*I over
     // |u| <= umax[|v|], one patch dword per lane and step (patch row v = window row v + 21,
     // patch dword c = window dword pd0 + c).  Byte i of dword c sits at u = base + i,
@@ -1581,6 +1552,41 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
                 const int T = (int)__builtin_amdgcn_udot4(pm, 0x03020100u, 0u, false);
                 m10 += __mul24(4 * c - sh - HALF_PATCH, S) + T;  // 24-bit multiplies: full-rate VALU
                 m01 += __mul24(r - HALF_PATCH, S);
+            }
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // IC's window reads before the overlay writes
+    // row pass: task = (4 window rows = 2 row pairs, group of 4 columns); window row r = level row
+    // y-21+r, sum column hc = level column x-18+hc; its 7 input bytes start at window byte
+    // x-5-xa+hc.  The sums overlay the window (Hs = window + OD_HOFF): the first 64 tasks take
+    // the lower row blocks (rq 10 .. 4), whose writes (from byte OD_HOFF + 160 * 8) only land
+    // on window rows >= 22, already read; the second round reads rows 0 .. 19 (LDS is in order
+    // per wave, and a task's reads precede its writes).
+    {
+        const int o0 = x - 5 - xa;  // 0..15, wave-uniform
+        const int sb = o0 & 3, sd = o0 >> 2;
+        const uint32_t* W32 = (const uint32_t*)W;
+        for (int task = lane; task < (OD_HPR / 2) * (OD_HC / 4); task += 64) {
+            const int rt = task / (OD_HC / 4), gq = task - rt * (OD_HC / 4);
+            const int rq = OD_HPR / 2 - 1 - rt;
+            uint32_t h[4][4];
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) {
+                const int r = min(4 * rq + s2, 2 * OD_WR);  // row 43 pads the last pair (tap 0)
+                // bytes 0 .. 9 of the span (byte 9 lies in d3 when sb == 3)
+                const uint32_t* q = W32 + r * (OD_WP / 4) + gq + sd;
+                const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3];
+                hrow4(__builtin_amdgcn_alignbyte(d1, d0, sb), __builtin_amdgcn_alignbyte(d2, d1, sb),
+                      __builtin_amdgcn_alignbyte(d3, d2, sb), h[s2]);
+            }
+#pragma unroll
+            for (int pr = 0; pr < 2; ++pr) {
+                uint4 o;
+                o.x = h[2 * pr][0] | (h[2 * pr + 1][0] << 16);
+                o.y = h[2 * pr][1] | (h[2 * pr + 1][1] << 16);
+                o.z = h[2 * pr][2] | (h[2 * pr + 1][2] << 16);
+                o.w = h[2 * pr][3] | (h[2 * pr + 1][3] << 16);
+                *(uint4*)(Hs + (2 * rq + pr) * OD_HC + 4 * gq) = o;
             }
         }
     }
@@ -1618,7 +1624,8 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
         uint32_t v = blur_round(T, tailAny && x + dx >= lg.xsimd_blur);
         if (edge) {
             const int X = x + dx, Y = y + dy;
-            if (X < 0 || X >= lg.w || Y < 0 || Y >= lg.h) v = W[(dy + OD_WR) * OD_WP + (x + dx + EDGE - xa)];
+            if (X < 0 || X >= lg.w || Y < 0 || Y >= lg.h)  // the window is overlaid: the padded level itself
+                v = pyr[lg.base + (long long)b * lg.fstride + (long long)(Y + EDGE) * lg.pitch + (X + EDGE)];
         }
         vals[q] = (int)v;
     }

@@ -10,16 +10,21 @@ import time
 sys.path.insert(0, str(pathlib.Path(__file__).resolve().parents[1]))
 import torch  # noqa: E402
 
-import orbslam_jpminipc_amd as orb  # noqa: E402
-from orbslam_jpminipc_amd.pipeline import FrontEndPipeline  # noqa: E402
-
 ap = argparse.ArgumentParser()
 ap.add_argument("--batch", type=int, default=512)
 ap.add_argument("--width", type=int, default=640)
 ap.add_argument("--height", type=int, default=480)
 ap.add_argument("--nfeatures", type=int, default=1000)
 ap.add_argument("--streams", default="1,2,3,4,8")
+ap.add_argument("--lib", default=None, help="a liborb_hip.so build to load instead of the in-tree one")
 a = ap.parse_args()
+if a.lib:
+    from orbslam_jpminipc_amd import _native  # noqa: E402
+
+    _native.HIP_LIB_PATH = pathlib.Path(a.lib).resolve()
+import orbslam_jpminipc_amd as orb  # noqa: E402
+from orbslam_jpminipc_amd.pipeline import FrontEndPipeline  # noqa: E402
+
 B, W, H, NF = a.batch, a.width, a.height, a.nfeatures
 frames = torch.from_numpy(orb.synth_stream(W, H, stream=0, first=0, count=B)).cuda()
 res = {}
@@ -40,4 +45,4 @@ for S in [int(x) for x in a.streams.split(",")]:
     torch.cuda.synchronize()
     res[S] = round((time.perf_counter() - t0) / 20 * 1e3, 4)
     pipe.close()
-print(json.dumps({"workload": [W, H, NF, B], "ms_per_step_by_streams": res}))
+print(json.dumps({"workload": [W, H, NF, B], "lib": a.lib, "ms_per_step_by_streams": res}))
