@@ -1120,7 +1120,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
 #define FT_IN_P 288           // staged row pitch (bytes): level columns x0-16 .. x0+271 (18 x 16 B)
 #define FT_IN_R (FT_H + 8)    // staged rows y0-4 .. y0+FT_H+3
 #define FT_SPW 264            // strength-plane row pitch (bytes): tile columns -4 .. 259
+#ifndef FT_Q
 #define FT_Q 512              // per-wave queue (u16 entries): lane-rows, then the NMS corner list
+#endif
 #define FT_CQ 320             // per-wave pixel list (u16 entries): < 64 carried + 256 expanded
 struct FastTile {
     int level, x0, y0;  // detection origin in level coordinates: x0 = 16 + 256 k, y0 = 16 + FT_H m
@@ -3008,12 +3010,15 @@ int orb_search_for_initialization_batch_device(const orb_keypoint_t* d_kps, cons
     if (bounds.max_x <= bounds.min_x || bounds.max_y <= bounds.min_y) return set_err(ORB_EINVAL, "bad bounds");
     if (cap > MATCH_BIG_NMAX) return set_err(ORB_ENOTSUP, "more than 8192 keypoints per frame");
     // octave-0 keypoints per frame held in LDS by k_match_init.  The extractor keeps at most
-    // mnFeaturesPerLevel[0] of them (0.217 nFeatures at scale 1.2, 8 levels), so 0.225 of the
-    // capacity covers its output and leaves room for two or more work-groups per CU (640x480:
-    // 0.233 -> 0.129 ms for 511 pairs, 1241x376: 0.47 -> 0.26); any frame beyond (another
-    // producer, another scale factor) is redone exactly by k_match_init_big below.
-    const int nmax =
-        std::min({cap, 1024, std::max(MATCH_NMAX_MIN, (int)(((long long)cap * MATCH_NMAX_NUM / 40 + 31) & ~31))});
+    // mnFeaturesPerLevel[0] of them (0.217 nFeatures at scale 1.2, 8 levels), so when the pairs
+    // fill the chip, 0.225 of the capacity covers its output and leaves room for two or more
+    // work-groups per CU (640x480: 0.233 -> 0.129 ms for 511 pairs, 1241x376: 0.47 -> 0.26);
+    // any frame beyond (another producer, another scale factor) is redone exactly by
+    // k_match_init_big below.  Fewer pairs than CUs: one work-group per CU anyway, and the
+    // full capacity spares the per-frame path the fallback launch.
+    const int nmax = P < 256 ? std::min(cap, 1024)
+                             : std::min({cap, 1024, std::max(MATCH_NMAX_MIN,
+                                                             (int)(((long long)cap * MATCH_NMAX_NUM / 40 + 31) & ~31))});
     const size_t lds = match_lds_bytes(cap, nmax);
     const int nmaxBig = std::min(cap, MATCH_BIG_NMAX);
     const size_t ldsBig = match_big_lds_bytes(cap, nmaxBig);

@@ -193,3 +193,33 @@ def test_matchers_from_three_threads():
     for t in ts:
         t.join()
     assert not errors, errors
+
+
+def test_match_batch_reduced_capacity_fallback():
+    """Batches of >= 256 pairs size k_match_init's LDS for 0.225 x the keypoint capacity of
+    octave-0 keypoints.  scaleFactor 1.5 over 5 levels keeps 0.38 x nFeatures at level 0, so
+    every pair of a 301-pair batch overflows it and is redone by k_match_init_big: bit-exact."""
+    import torch
+
+    frames = orb.synth_stream(640, 480, stream=21, first=0, count=8)
+    ext = orb.ORBextractor(1000, 1.5, 5, orb.FAST_SCORE, 20, device=0, max_batch=8)
+    d_kps, d_desc, d_cnt = ext.extract_batch_device(torch.from_numpy(frames).cuda())
+    f1 = torch.tensor([b for _ in range(43) for b in range(7)], dtype=torch.int32, device="cuda")
+    m12, nm = orb.ORBmatcher(0.9, True).search_for_initialization_batch_device(d_kps, d_desc, d_cnt, f1, f1 + 1,
+                                                                               640, 480, 100)
+    torch.cuda.synchronize()
+    kps, desc, cnt = d_kps.cpu().numpy(), d_desc.cpu().numpy(), d_cnt.cpu().numpy()
+    m12, nm = m12.cpu().numpy(), nm.cpu().numpy()
+    ora = Oracle(1000, 1.5, 5, 1, 20)
+    ref = [ora.extract(f) for f in frames]
+    oct0 = [int((r[0]["octave"] == 0).sum()) for r in ref]
+    assert min(oct0) > 0.225 * ext.max_keypoints and min(oct0) > 256, oct0  # the fallback really runs
+    for b in range(8):
+        assert kps[b, : cnt[b]].tobytes() == ref[b][0].tobytes()
+    for p in range(len(f1)):
+        b = p % 7
+        k1, d1 = ref[b]
+        k2, d2 = ref[b + 1]
+        prev = np.ascontiguousarray(np.stack([k1["x"], k1["y"]], 1).astype(np.float32))
+        no, m12o = search_for_initialization(k1, d1, k2, d2, 640, 480, prev, 0.9, True, 100)
+        assert nm[p] == no and np.array_equal(m12[p, : cnt[b]], m12o), p
