@@ -805,6 +805,9 @@ __device__ __forceinline__ int cell_of(const int* off, int n, int i) {
 #ifndef KS_SEP_BATCH
 #define KS_SEP_BATCH 32  // batches below this re-run FAST(7) cells in k_rerun, not in k_select
 #endif
+#ifndef KS_CELL_SPREAD
+#define KS_CELL_SPREAD 1
+#endif
 #ifndef KS_SEP_PIXELS
 #define KS_SEP_PIXELS 400000  // and frames larger than this
 #endif
@@ -1010,7 +1013,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
         }
         __syncthreads();
         HarrisGreater hcomp;
-        for (int c = tid; c < nC; c += 256) {
+        for (int c = KS_CELL_SPREAD ? lane * 4 + wave : tid; c < nC; c += 256) {  // cell c on wave c % 4
             uint64_t* seg = hs + (inLds ? s_off[c] : lc[c].candOff);
             s_cnt[c] = orbsel::retain_best(seg, s_cnt[c], s_ret[c], hcomp);
         }
@@ -1049,7 +1052,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
     }
     // (4) retainBest per cell, then the level list in cell order, then retainBest to the quota
     ScoreGreater comp;
-    for (int c = tid; c < nC; c += 256) {
+    // cells dealt round-robin over the four waves (cell c on wave c % 4): a level's few dozen
+    // serial replays run on four SIMDs instead of one wave's lanes
+    for (int c = KS_CELL_SPREAD ? lane * 4 + wave : tid; c < nC; c += 256) {
         uint32_t* seg = srt + (inLds ? s_off[c] : lc[c].candOff);
         s_cnt[c] = KS_SKIP_RETAIN ? min(s_cnt[c], max(s_ret[c], 0)) : orbsel::retain_best(seg, s_cnt[c], s_ret[c], comp);
     }
