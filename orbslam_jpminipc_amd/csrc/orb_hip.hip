@@ -98,6 +98,7 @@ struct LevelGeom {
     int xs_resize, xmax;    // VResizeLinear SSE2 columns, HResizeLinear xmax (l >= 1)
     int rtab;               // offset of this level's resize table (int32 units), l >= 1
     int rtile;              // offset of this level's resize tile table (4 ints per tile), l >= 1
+    int rtileS;             // the same for the short tiles of small batches (RZ_THS rows)
     float scale;            // mvScaleFactor[l]
     float size;             // (int)(31 * mvScaleFactor[l])
     int cellW, cellH;       // detection-area size of the (non-last) cells: corner -> cell bucket
@@ -306,14 +307,21 @@ __device__ __forceinline__ void stage_rows_to_lds(uint32_t* __restrict__ dst, in
 #ifndef RZ_TH
 #define RZ_TH 32
 #endif
+#ifndef RZ_THS
+#define RZ_THS 4  // tile rows for batches below KR_SHORT_BATCH (B=1 640x480: 0.074 -> 0.035 ms for levels 1-7)
+#endif
+#ifndef KR_SHORT_BATCH
+#define KR_SHORT_BATCH 8
+#endif
 // The two levels arrive by value: a Geom indexed by the runtime level was copied to scratch
 // (144 B per lane of private-memory traffic per thread).
+template <int TH>
 __global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, const int* __restrict__ rtab,
                                                     const LevelGeom lg, const LevelGeom ls) {
     extern __shared__ __attribute__((aligned(16))) uint32_t s_src[];
     const int b = blockIdx.z, tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int* tt = rtab + lg.rtile + 4 * (blockIdx.y * gridDim.x + blockIdx.x);
+    const int* tt = rtab + (TH == RZ_TH ? lg.rtile : lg.rtileS) + 4 * (blockIdx.y * gridDim.x + blockIdx.x);
     const int colStart = tt[0], words = tt[1], rowMin = tt[2], nrows = tt[3];
     const uint8_t* S = pyr + ls.base + (long long)b * ls.fstride + (long long)EDGE * ls.pitch + EDGE;
     stage_tile16((uint4*)s_src, (const uint4*)(S + (long long)rowMin * ls.pitch + colStart), ls.pitch >> 4, nrows,
@@ -322,12 +330,12 @@ __global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, c
     const int* alpha = xofs + lg.w;
     const int* yofs = alpha + lg.w;
     const int* beta = yofs + lg.h;
-    // the wave's RZ_TH / 4 row coefficients, one row per lane, fetched while the tile loads
+    // the wave's TH / 4 row coefficients, one row per lane, fetched while the tile loads
     // (read back with readlane: no dependent global load inside the row walk)
-    const int pyA = blockIdx.y * RZ_TH + wave * (RZ_TH / 4);
-    const int pyB = min(pyA + RZ_TH / 4, lg.ph);
+    const int pyA = blockIdx.y * TH + wave * (TH / 4);
+    const int pyB = min(pyA + TH / 4, lg.ph);
     int rowSy = 0, rowBeta = 0;
-    if (lane < RZ_TH / 4 && pyA + lane < pyB) {
+    if (lane < TH / 4 && pyA + lane < pyB) {
         const int ly = reflect101(pyA + lane - EDGE, lg.h);
         rowSy = yofs[ly];
         rowBeta = beta[ly];
@@ -2150,7 +2158,7 @@ struct orb_extractor {
     std::vector<CellGeom> cells;
     std::vector<int> rtab;
     size_t cellLds = 0, selectLds = 0;  // a FAST(7) re-run's LDS (largest cell); k_select's
-    size_t resizeLds[ORB_MAX_LEVELS] = {};
+    size_t resizeLds[ORB_MAX_LEVELS] = {}, resizeLdsS[ORB_MAX_LEVELS] = {};
     int resizeTail = 0;           // first level of k_pyr_resize_tail (nlevels: none)
     int tailBufA = 0, tailBufB = 0;
     size_t tailLds = 0;
@@ -2453,34 +2461,39 @@ struct orb_extractor {
             rt.insert(rt.end(), alpha.begin(), alpha.end());
             rt.insert(rt.end(), yofs.begin(), yofs.end());
             rt.insert(rt.end(), beta.begin(), beta.end());
-            // source rectangle of every RZ_TW x RZ_TH tile of the padded level (k_pyr_resize)
-            const int tx = (lg.pitch + RZ_TW - 1) / RZ_TW, ty = (lg.ph + RZ_TH - 1) / RZ_TH;
-            lg.rtile = (int)rt.size();
-            size_t lds = 0;
-            for (int y = 0; y < ty; ++y)
-                for (int x = 0; x < tx; ++x) {
-                    int c0 = INT32_MAX, c1 = -1, r0 = INT32_MAX, r1 = -1;
-                    for (int px = x * RZ_TW; px < std::min((x + 1) * RZ_TW, lg.pitch); ++px) {
-                        const int lx = orbdev::reflect101(std::min(px, dw + 31) - 16, dw);
-                        const int sx = xofs[lx];
-                        const int sx1 = (lx < xmax && (alpha[lx] >> 16) != 0) ? sx + 1 : sx;
-                        c0 = std::min(c0, sx);
-                        c1 = std::max(c1, sx1);
+            // source rectangle of every RZ_TW x TH tile of the padded level (k_pyr_resize), for
+            // the two tile heights
+            auto tiles = [&](int TH, int& off, size_t& ldsOut) {
+                const int tx = (lg.pitch + RZ_TW - 1) / RZ_TW, ty = (lg.ph + TH - 1) / TH;
+                off = (int)rt.size();
+                size_t lds = 0;
+                for (int y = 0; y < ty; ++y)
+                    for (int x = 0; x < tx; ++x) {
+                        int c0 = INT32_MAX, c1 = -1, r0 = INT32_MAX, r1 = -1;
+                        for (int px = x * RZ_TW; px < std::min((x + 1) * RZ_TW, lg.pitch); ++px) {
+                            const int lx = orbdev::reflect101(std::min(px, dw + 31) - 16, dw);
+                            const int sx = xofs[lx];
+                            const int sx1 = (lx < xmax && (alpha[lx] >> 16) != 0) ? sx + 1 : sx;
+                            c0 = std::min(c0, sx);
+                            c1 = std::max(c1, sx1);
+                        }
+                        for (int py = y * TH; py < std::min((y + 1) * TH, lg.ph); ++py) {
+                            const int ly = orbdev::reflect101(py - 16, dh);
+                            r0 = std::min(r0, std::min(std::max(yofs[ly], 0), sh - 1));
+                            r1 = std::max(r1, std::min(std::max(yofs[ly] + 1, 0), sh - 1));
+                        }
+                        const int cs = c0 & ~15, units = ((c1 - cs) >> 4) + 1, nr = r1 - r0 + 1;
+                        rt.push_back(cs);
+                        rt.push_back(units);
+                        rt.push_back(r0);
+                        rt.push_back(nr);
+                        lds = std::max(lds, (size_t)units * 16 * nr);
                     }
-                    for (int py = y * RZ_TH; py < std::min((y + 1) * RZ_TH, lg.ph); ++py) {
-                        const int ly = orbdev::reflect101(py - 16, dh);
-                        r0 = std::min(r0, std::min(std::max(yofs[ly], 0), sh - 1));
-                        r1 = std::max(r1, std::min(std::max(yofs[ly] + 1, 0), sh - 1));
-                    }
-                    const int cs = c0 & ~15, units = ((c1 - cs) >> 4) + 1, nr = r1 - r0 + 1;
-                    rt.push_back(cs);
-                    rt.push_back(units);
-                    rt.push_back(r0);
-                    rt.push_back(nr);
-                    lds = std::max(lds, (size_t)units * 16 * nr);
-                }
-            if (lds > 96 * 1024) return set_err(ORB_ENOTSUP, "scale factor too large for the resize tile");
-            resizeLds[l] = lds;
+                ldsOut = lds;
+            };
+            tiles(RZ_TH, lg.rtile, resizeLds[l]);
+            tiles(RZ_THS, lg.rtileS, resizeLdsS[l]);
+            if (resizeLds[l] > 96 * 1024) return set_err(ORB_ENOTSUP, "scale factor too large for the resize tile");
         }
         // the fused small-level tail: the first level from which every later level's source
         // ROI (ping-pong A / B) plus the staged tables fit the CU's LDS
@@ -2677,8 +2690,15 @@ struct orb_extractor {
         const int tail = B < KR_TAIL_BATCH ? nlevels : resizeTail;
         for (int l = 1; l < tail; ++l) {
             const LevelGeom& lg = g.lv[l];
-            dim3 grid((lg.pitch + RZ_TW - 1) / RZ_TW, (lg.ph + RZ_TH - 1) / RZ_TH, B);
-            hipLaunchKernelGGL(k_pyr_resize, grid, dim3(256), resizeLds[l], st, d_pyr, d_rtab, g.lv[l], g.lv[l - 1]);
+            if (B < KR_SHORT_BATCH) {
+                dim3 grid((lg.pitch + RZ_TW - 1) / RZ_TW, (lg.ph + RZ_THS - 1) / RZ_THS, B);
+                hipLaunchKernelGGL(k_pyr_resize<RZ_THS>, grid, dim3(256), resizeLdsS[l], st, d_pyr, d_rtab, g.lv[l],
+                                   g.lv[l - 1]);
+            } else {
+                dim3 grid((lg.pitch + RZ_TW - 1) / RZ_TW, (lg.ph + RZ_TH - 1) / RZ_TH, B);
+                hipLaunchKernelGGL(k_pyr_resize<RZ_TH>, grid, dim3(256), resizeLds[l], st, d_pyr, d_rtab, g.lv[l],
+                                   g.lv[l - 1]);
+            }
         }
         if (tail < nlevels)
             hipLaunchKernelGGL(k_pyr_resize_tail, dim3(B), dim3(RT_THREADS), tailLds, st, d_pyr, d_rtab, g, resizeTail,
