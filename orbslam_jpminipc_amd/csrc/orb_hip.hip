@@ -739,7 +739,11 @@ struct ScoreGreater {  // KeypointResponseGreater on the packed FAST score
 // (4) retainBest per cell, concatenation in cell order, retainBest to the level quota
 // (ORBextractor.cc:680-701) — exact libstdc++ nth_element replays.  Lists live in LDS when the
 // level's survivors fit (SELECT_CAP), otherwise in the frame's scratch area `cand2`.
-#define SELECT_CAP 6144
+#ifndef SELECT_CAP
+#define SELECT_CAP 3072  // survivors per level held in LDS (a few hundred to ~2000 at every
+                         // BASELINE size; beyond: the global-scratch path).  24 KB lets 6
+                         // work-groups share a CU (6144: 3): KITTI 0.70 -> 0.55 ms, 720p 1.33 -> 1.20
+#endif
 // KeypointResponseGreater on HARRIS_SCORE elements: float response in the high word, the
 // packed FAST record (identity) in the low word.
 struct HarrisGreater {
@@ -959,9 +963,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
     }
     __syncthreads();
     const int M = s_off[nC];
-    const bool inLds = M <= SELECT_CAP;
+    constexpr int selCap = SELECT_CAP;
+    const bool inLds = M <= selCap;
     uint32_t* raw = (uint32_t*)smem;                                      // arrival order
-    uint32_t* srt = inLds ? raw + SELECT_CAP : cand2 + (long long)b * g.candPerFrame;  // raster order
+    uint32_t* srt = inLds ? raw + selCap : cand2 + (long long)b * g.candPerFrame;  // raster order
     const uint32_t* srcOf = inLds ? raw : fcand;
     if (inLds) {  // the level's survivors, cell after cell, one element per thread (4 loads in flight)
         for (int i0 = tid; i0 < M; i0 += 1024) {
@@ -1009,7 +1014,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
     if constexpr (HARRIS) {
         // HarrisResponses on every cell keypoint (ORBextractor.cc:616-620), then the same
         // retention on (response, record) pairs
-        uint64_t* hs = inLds ? (uint64_t*)(smem + (size_t)8 * SELECT_CAP) : candH + (long long)b * g.candPerFrame;
+        uint64_t* hs = inLds ? (uint64_t*)(smem + (size_t)8 * selCap) : candH + (long long)b * g.candPerFrame;
         const uint8_t* roi = pyr + lg.base + (long long)b * lg.fstride + (long long)EDGE * lg.pitch + EDGE;
         for (int c = wave; c < nC; c += 4) {
             const int o = inLds ? s_off[c] : lc[c].candOff;
