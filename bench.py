@@ -473,6 +473,14 @@ def run_rank(args):
             "GBps": nbytes / (per_launch_ms * 1e-3) / 1e9 if per_launch_ms > 0 else None,
             "measured_in": "timed region" if name == dom else "survey pass",
         }
+    # batches >= 256 frames build the whole pyramid in one k_pyr_stream launch (profile stage 0,
+    # stage 1 empty): its algorithmic bytes are the level-0 read and the derived levels written
+    if "k_pyr0" in stages and "k_pyr_resize" not in stages:
+        s = stages.pop("k_pyr0")
+        s["bytes_per_launch"] = B * sum(px)
+        s["GBps"] = s["bytes_per_launch"] / (s["ms_per_launch"] * 1e-3) / 1e9
+        s["note"] = "whole pyramid (level-0 read + levels 1-7 written) in one streaming launch"
+        stages = {"k_pyr_stream": s, **stages}
     # the resize stage builds levels 1-7 (k_pyr_resize per large level, the small levels in one
     # k_pyr_resize_tail launch): report per-level numbers
     if "k_pyr_resize" in stages:

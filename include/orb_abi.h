@@ -446,6 +446,14 @@ int orb_debug_blur_image(orb_extractor_t* h, int b, int l, uint8_t* out);
  * three zeros. */
 int orb_debug_klevel_counts(unsigned long long* out3);
 int orb_debug_cell_counts(orb_extractor_t* h, int b, int l, int* counts, int cap);
+/* Pyramid kernels used by the next extractions (results are identical): 0 = automatic (the
+ * one-pass streaming kernel k_pyr_stream for batches >= 256 grey frames, per-level launches
+ * otherwise), 1 = per-level launches always, 2 = k_pyr_stream at every batch size of grey
+ * frames whenever the current geometry has a stream plan. */
+int orb_debug_set_pyramid_path(orb_extractor_t* h, int mode);
+/* The current geometry's k_pyr_stream plan: returns 1 (and level-0 rows per round, rounds,
+ * LDS bytes) when there is one, 0 when the geometry only runs per-level launches. */
+int orb_debug_pyramid_plan(const orb_extractor_t* h, int* rows_per_round, int* rounds, int* lds_bytes);
 
 #ifdef __cplusplus
 }

@@ -529,6 +529,321 @@ __global__ void __launch_bounds__(RT_THREADS) k_pyr_resize_tail(uint8_t* __restr
     }
 }
 
+// ---- the whole pyramid of a frame in one streaming pass (large batches) ------------------
+// k_pyr0 + k_pyr_resize x (L-1) read every level l-1 back from HBM to build level l.  Here one
+// 1024-thread workgroup per frame walks down the frame once: each round loads the next K0
+// level-0 rows into an LDS ring (prefetched into registers during the previous round), and
+// every level l >= 1 computes the rows whose two source rows of level l-1 are already in that
+// level's ring, writing them to the padded pyramid and (for the next level) to its own ring.
+// Level l works on rows its source finished in an earlier round (level 1 on the level-0 rows of
+// this round), so all levels run in one task pool per round: two barriers per round, no
+// intermediate level ever leaves the CU except as the pyramid itself.  HBM traffic = the input
+// read once + every padded level written once.
+// The task loop issues no global load: on CDNA the vector-memory counter also counts stores, so
+// a table load after a row's stores would wait for them.  The per-column taps live in LDS
+// for the whole kernel, and the row entries of round n+1 are staged with the level-0 prefetch.
+// The round schedule, ring capacities (the oldest row any round still reads to the newest one
+// written by then), ring slots of every row and the per-column resize taps are host-built
+// (build_stream_plan); the arithmetic per padded pixel is k_pyr0's / k_pyr_resize's exactly.
+// Every ROI row r of a level goes to padded row r + 16 and to its reflect-101 mirrors 16 - r
+// (1 <= r <= 16) and 2h + 14 - r (h - 17 <= r <= h - 2); the host requires h, w >= 17.
+struct StreamLevel {
+    int nq;             // tasks per row: 16-B chunks (level 0) / 4-px quads (l >= 1) of the padded row
+    uint32_t nqm;       // ceil(2^32 / nq): row = umulhi(task, nqm) (exact for the task counts used)
+    int ringOff;        // LDS byte offset of the level's ring of ROI rows (levels < L-1)
+    int ringPitch;      // its row pitch (bytes, multiple of 16)
+    int colOff;         // LDS byte offset of the level's column words (l >= 1; 16 B per quad)
+    int waveStart, nWaves;  // the workgroup's waves that build this level
+    int w, h, pitch;
+    long long base, fstride;
+};
+struct StreamGeom {
+    int L, nRounds;
+    int u0;             // 16-B units per level-0 ROI row
+    uint32_t u0m;       // ceil(2^32 / u0)
+    int align;          // input alignment: 16 / 4 / 1 (pointer, stride and frame pitch)
+    int colWords;       // u32 column words of all levels (LDS-resident)
+    int colOff;         // LDS byte offset of the column words
+    int rowOff;         // LDS byte offset of the two row-entry stages (rowStride uint2 each)
+    int rowStride;      // row entries per stage (the most any round has)
+    int cap0;           // level-0 ring rows (row r in slot r % cap0)
+};
+#define PS_THREADS 1024
+#define PS_LOADERS 2  // loader waves per workgroup
+#define PS_NPF 8     // level-0 units (and row entries) per loader lane and round: K0 * u0 <= 1024
+#ifndef KR_STREAM_BATCH  // smallest batch that uses k_pyr_stream (one workgroup per frame)
+#define KR_STREAM_BATCH 256
+#endif
+#define PS_LDS_TARGET (76 * 1024)  // two workgroups per CU
+
+__device__ __forceinline__ uint4 load_unit16(const uint8_t* p, int nvalid, int align) {
+    if (nvalid >= 16 && align == 16) return *(const uint4*)p;
+    if (nvalid >= 16 && align == 4) {
+        const uint32_t* q = (const uint32_t*)p;
+        return make_uint4(q[0], q[1], q[2], q[3]);
+    }
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        if (k < nvalid) w[k >> 2] |= (uint32_t)p[k] << (8 * (k & 3));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+typedef unsigned short ps_u16x2 __attribute__((ext_vector_type(2)));
+// high 32 bits of the 48-bit product of two 24-bit operands (v_mul_hi_u32_u24)
+__device__ __forceinline__ uint32_t mulhi24(uint32_t a, uint32_t b) {
+    return (uint32_t)(((uint64_t)(a & 0xFFFFFFu) * (uint64_t)(b & 0xFFFFFFu)) >> 32);
+}
+// LDS-only barrier: the ring and stage hand-offs are LDS; the pyramid stores need not drain
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+#ifndef PS_TIMING  // 1: per-phase s_memtime sums of k_pyr_stream's waves (experiment builds only)
+#define PS_TIMING 0
+#endif
+#if PS_TIMING
+__device__ unsigned long long g_pstime[32];
+#define PS_T(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#else
+#define PS_T(v)
+#endif
+// rounds[n]: per level lo | cnt << 12 | (first stage entry) << 18 (L words), then the round's
+// first row entry in rowEntries and the round's entry count
+#ifndef PS_WAVES
+#define PS_WAVES 8  // waves per SIMD the register allocation targets (two workgroups per CU)
+#endif
+#define PS_LB 4  // level-0 units per loader lane in flight at once
+#ifndef PS_EXP  // timing experiments only (wrong output): 1 builders idle, 2 no pyramid stores, 3 no input loads
+#define PS_EXP 0
+#endif
+__global__ void __launch_bounds__(PS_THREADS) __attribute__((amdgpu_waves_per_eu(PS_WAVES)))
+k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uint8_t* __restrict__ pyr,
+             const uint32_t* __restrict__ colWords, const uint2* __restrict__ rowEntries,
+             const StreamLevel* __restrict__ slv, const uint32_t* __restrict__ rounds, StreamGeom sg) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t s_ring[];
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const int rw = sg.L + 2;  // words per round record
+    uint2* stage = (uint2*)(s_ring + sg.rowOff);
+    for (int i = tid; i < sg.colWords; i += PS_THREADS) ((uint32_t*)(s_ring + sg.colOff))[i] = colWords[i];
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+    // The first PS_LOADERS waves are loaders: during round n they bring the level-0 rows and
+    // the row entries of round n+1 into the ring (whose capacity covers one round ahead) and
+    // the other stage, while every other wave builds its level's rows of round n; one barrier
+    // per round hands both over.  Builder waves hold no prefetch registers.
+    if (wave < PS_LOADERS) {
+        const uint8_t* img = imgs + (long long)b * fpitch;
+        const int w0 = slv[0].w, r0Off = slv[0].ringOff, r0Pitch = slv[0].ringPitch;
+        for (int n = 0; n <= sg.nRounds; ++n) {
+            if (n < sg.nRounds) {
+                const uint32_t e = rounds[n * rw];
+                const int lo = e & 0xFFF, units = (int)((e >> 12) & 0x3F) * sg.u0;
+                const int eFirst = rounds[n * rw + sg.L], ne = rounds[n * rw + sg.L + 1];
+                for (int i0 = tid; i0 < units; i0 += PS_LB * 64 * PS_LOADERS) {
+                    uint4 pf[PS_LB];
+#pragma unroll
+                    for (int k = 0; k < PS_LB; ++k) {
+                        const int i = i0 + k * 64 * PS_LOADERS;
+                        if (i < units) {
+                            const int r = (int)__umulhi((uint32_t)i, sg.u0m), u = i - r * sg.u0;
+                            pf[k] = PS_EXP == 3 ? make_uint4(r, u, 0, 0) : load_unit16(img + (long long)(lo + r) * stride + 16 * u, w0 - 16 * u, sg.align);
+                        }
+                    }
+#pragma unroll
+                    for (int k = 0; k < PS_LB; ++k) {
+                        const int i = i0 + k * 64 * PS_LOADERS;
+                        if (i < units) {
+                            const int r = (int)__umulhi((uint32_t)i, sg.u0m), u = i - r * sg.u0;
+                            *(uint4*)(s_ring + r0Off + ((lo + r) % sg.cap0) * r0Pitch + 16 * u) = pf[k];
+                        }
+                    }
+                }
+                for (int i = tid; i < ne; i += 64 * PS_LOADERS) stage[(n & 1) * sg.rowStride + i] = rowEntries[eFirst + i];
+            }
+            lds_barrier();  // round n's data is in LDS (n = 0: before the first round)
+        }
+        return;
+    }
+    // builder waves: this wave's level (host-assigned wave groups) and its column units
+    int myL = 0;
+    for (int l = 0; l < sg.L; ++l)
+        if (wave >= slv[l].waveStart && wave < slv[l].waveStart + slv[l].nWaves) myL = l;
+    const int ws = slv[myL].waveStart, nWaves = slv[myL].nWaves;
+    const bool idle = wave < ws || wave >= ws + nWaves;  // a wave no level needed
+    const int nq = slv[myL].nq, w = slv[myL].w, h = slv[myL].h, pitch = slv[myL].pitch;
+    const int ownOff = slv[myL].ringOff, ownPitch = slv[myL].ringPitch, colOff = slv[myL].colOff;
+    const int srcOff = slv[myL > 0 ? myL - 1 : 0].ringOff, srcPitch = slv[myL > 0 ? myL - 1 : 0].ringPitch;
+    uint8_t* D = pyr + slv[myL].base + (long long)b * slv[myL].fstride;
+    const int ql = (wave - ws) * 64 + lane, qs = 64 * nWaves;
+    const int mirBot = h - 17;  // rows >= mirBot (and <= h-2) have a bottom mirror
+    lds_barrier();
+#if PS_TIMING
+    unsigned long long acc[5] = {0, 0, 0, 0, 0};
+#endif
+    for (int n = 0; n < sg.nRounds; ++n) {
+        PS_T(t1);
+        const uint32_t e = idle ? 0u : rounds[n * rw + myL];
+        const int lo = e & 0xFFF, cnt = PS_EXP == 1 ? 0 : (e >> 12) & 0x3F;
+        const uint2* E = stage + (n & 1) * sg.rowStride + (e >> 18);
+        if (cnt > 0 && myL == 0) {
+            // padded level-0 rows from the ring (k_pyr0's copyMakeBorder), 16 B per unit
+            for (int c = ql; c < nq; c += qs) {
+                const int px = 16 * c;
+                const bool inner = px >= EDGE && px <= w;
+                uint8_t* Dc = D + px;
+                for (int k = 0; k < cnt; ++k) {
+                    const int r = lo + k;
+                    const int slot = __builtin_amdgcn_readfirstlane((int)(E[k].x >> 16));
+                    const uint8_t* R = s_ring + ownOff + slot * ownPitch;
+                    uint4 v;
+                    if (inner) {
+                        v = *(const uint4*)(R + px - EDGE);
+                    } else {  // a border unit: single-bounce reflect-101 (w >= 17); all 16
+                              // reads unconditional (clamped), so they issue back to back
+                        uint32_t by[16];
+#pragma unroll
+                        for (int j = 0; j < 16; ++j) {
+                            const int X = min(px + j - EDGE, w + EDGE - 1);
+                            by[j] = R[X < 0 ? -X : (X >= w ? 2 * w - 2 - X : X)];
+                        }
+                        uint32_t w4[4];
+#pragma unroll
+                        for (int q4 = 0; q4 < 4; ++q4) {
+                            uint32_t word = 0;
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) word |= (px + 4 * q4 + j < w + 2 * EDGE ? by[4 * q4 + j] : 0u) << (8 * j);
+                            w4[q4] = word;
+                        }
+                        v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
+                    }
+                    if (PS_EXP == 2) {
+                        if (v.x == 0x12345678u) *(uint4*)Dc = v;
+                        continue;
+                    }
+                    *(uint4*)(Dc + __mul24(r + EDGE, pitch)) = v;
+                    if (r >= 1 && r <= EDGE) *(uint4*)(Dc + __mul24(EDGE - r, pitch)) = v;
+                    if (r >= mirBot && r <= h - 2) *(uint4*)(Dc + __mul24(2 * h + 14 - r, pitch)) = v;
+                }
+            }
+        } else if (cnt > 0) {
+            // level myL from the ring of level myL-1: per column unit, the round's rows in order
+            const uint4* C = (const uint4*)(s_ring + colOff);
+            for (int q = ql; q < nq; q += qs) {
+                // column words: sx | a1 << 12 | (a0 - 2047 + a1) << 24 | simd << 26 | live << 27
+                const uint4 cw = C[q];
+                const uint32_t cc[4] = {cw.x, cw.y, cw.z, cw.w};
+                int sx[4];
+                uint32_t ap[4], live = 0, simd = 0;  // ap = a0 | a1 << 16 (v_dot2 operand)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    sx[j] = (int)(cc[j] & 0xFFFu);
+                    const uint32_t a1 = (cc[j] >> 12) & 0xFFFu;
+                    ap[j] = (2047u + ((cc[j] >> 24) & 3u) - a1) | (a1 << 16);
+                    if (cc[j] & (1u << 26)) simd |= 1u << j;
+                    if (cc[j] & (1u << 27)) live |= 0xFFu << (8 * j);
+                }
+                const bool allSimd = simd == 0xFu;
+                // HResizeLinear of source row `slot`: H = S[sx] a0 + S[sx+1] a1 (a1 == 0 where
+                // OpenCV reads S[sx] only: the byte after it is multiplied by 0; it lies in the
+                // ring row's slack or the next LDS row, never outside the allocation).  On
+                // all-SSE2 quads h keeps (H >> 4) << 8 for the v_mul_hi_u32_u24 below.
+                auto hrow = [&](int slot, uint32_t* hh) {
+                    const uint8_t* R = s_ring + srcOff + slot * srcPitch;
+                    uint32_t lo8[4], hi8[4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        lo8[j] = R[sx[j]];
+                        hi8[j] = R[sx[j] + 1];
+                    }
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const uint32_t H = __builtin_amdgcn_udot2(__builtin_bit_cast(ps_u16x2, lo8[j] | (hi8[j] << 16)),
+                                                                  __builtin_bit_cast(ps_u16x2, ap[j]), 0u, false);
+                        hh[j] = allSimd ? ((H << 4) & 0xFFFFFF00u) : H;
+                    }
+                };
+                const int cx = 4 * q - EDGE;
+                const bool roi = cx >= 0 && cx < w;
+                uint8_t* Dc = D + 4 * q;
+                int sA = -1, sB = -1;
+                uint32_t hA[4] = {0u, 0u, 0u, 0u}, hB[4] = {0u, 0u, 0u, 0u};
+                for (int k = 0; k < cnt; ++k) {
+                    const int dy = lo + k;
+                    // entry (wave-uniform): slot0 | slot1 << 8 | own << 16 (0xFFFF: none), beta
+                    const uint2 en0 = E[k];
+                    const uint32_t ex = __builtin_amdgcn_readfirstlane(en0.x), ey = __builtin_amdgcn_readfirstlane(en0.y);
+                    const int s0 = (int)(ex & 0xFFu), s1 = (int)((ex >> 8) & 0xFFu);
+                    if (s0 != sA) {
+                        if (s0 == sB) {
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) hA[j] = hB[j];
+                        } else {
+                            hrow(s0, hA);
+                        }
+                        sA = s0;
+                    }
+                    if (s1 != sB) {
+                        if (s1 == sA) {
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) hB[j] = hA[j];
+                        } else {
+                            hrow(s1, hB);
+                        }
+                        sB = s1;
+                    }
+                    const uint32_t b0 = ey & 0xFFFFu, b1 = ey >> 16;
+                    uint32_t word = 0;
+                    if (allSimd) {
+                        // VResizeLinearVec_32s8u: ((H >> 4) * b) >> 16 per term = the high 32 bits of
+                        // ((H >> 4) << 8) * (b << 8) (both < 2^24), + 2 >> 2
+                        const uint32_t B0 = b0 << 8, B1 = b1 << 8;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            word |= ((mulhi24(hA[j], B0) + mulhi24(hB[j], B1) + 2u) >> 2) << (8 * j);
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const uint32_t r = ((simd >> j) & 1u)
+                                                   ? ((__umul24(hA[j] >> 4, b0) >> 16) + (__umul24(hB[j] >> 4, b1) >> 16) + 2u) >> 2
+                                                   : (__umul24(hA[j], b0) + __umul24(hB[j], b1) + (1u << 21)) >> 22;
+                            word |= r << (8 * j);
+                        }
+                    }
+                    word &= live;
+                    if (PS_EXP != 2) {
+                        *(uint32_t*)(Dc + __mul24(dy + EDGE, pitch)) = word;
+                        if (dy >= 1 && dy <= EDGE) *(uint32_t*)(Dc + __mul24(EDGE - dy, pitch)) = word;
+                        if (dy >= mirBot && dy <= h - 2) *(uint32_t*)(Dc + __mul24(2 * h + 14 - dy, pitch)) = word;
+                    } else if (word == 0x12345678u) {
+                        *(uint32_t*)Dc = word;
+                    }
+                    const int own = (int)(ex >> 16);
+                    if (own != 0xFFFF && roi) *(uint32_t*)(s_ring + ownOff + __mul24(own, ownPitch) + cx) = word;
+                }
+            }
+        }
+        PS_T(t2);
+        lds_barrier();
+#if PS_TIMING
+        PS_T(t3);
+        acc[1] += t2 - t1;
+        acc[2] += t3 - t2;
+#endif
+    }
+#if PS_TIMING
+    if (lane == 0) {
+        for (int k = 0; k < 5; ++k) atomicAdd(&g_pstime[k], acc[k]);
+        atomicAdd(&g_pstime[5], 1ull);
+        if (!idle) {
+            atomicAdd(&g_pstime[8 + myL], acc[1]);
+            atomicAdd(&g_pstime[24 + myL], 1ull);
+        }
+    }
+#endif
+}
+
 // ---- FAST strength --------------------------------------------------------------------------
 // S(p) = 1 + cornerScore<16>(p) of cv::FAST: the largest t for which p is a corner is S - 1,
 // so p is a corner at threshold t <=> S > t; records carry S - 1 as the score.
@@ -2167,6 +2482,15 @@ struct orb_extractor {
     int resizeTail = 0;           // first level of k_pyr_resize_tail (nlevels: none)
     int tailBufA = 0, tailBufB = 0;
     size_t tailLds = 0;
+    // k_pyr_stream plan (build_stream_plan); streamOk false: per-level launches only
+    bool streamOk = false;
+    StreamGeom sgeom{};
+    size_t streamLds = 0;
+    int streamK0 = 0;
+    uint32_t* d_scol = nullptr;
+    uint2* d_srows = nullptr;
+    StreamLevel* d_slv = nullptr;
+    uint32_t* d_srounds = nullptr;
     // device workspace
     uint8_t* d_pyr = nullptr;
     FastTile* d_tiles = nullptr;
@@ -2187,6 +2511,8 @@ struct orb_extractor {
     // bit 0 = pyramid (stages 0-1), bit 1 = detection, selection and descriptors (stages 2-4,
     // reading the pyramid bit 0 left in the workspace)
     unsigned phaseMask = 3u;
+    bool pyrLegacy = false;        // orb_debug_set_pyramid_path(1): per-level launches at every batch size
+    bool pyrStreamAlways = false;  // orb_debug_set_pyramid_path(2): k_pyr_stream at every batch size
     bool prof = false;
     unsigned profMask = 0;           // stages that record events (bit k = stage k)
     std::vector<hipEvent_t> evPool;  // 2 per stage per launch, recycled after each read
@@ -2233,7 +2559,16 @@ struct orb_extractor {
         hipFree(d_img);
         hipFree(d_imgColor);
         hipFree(d_out);
+        hipFree(d_scol);
+        hipFree(d_srows);
+        hipFree(d_slv);
+        hipFree(d_srounds);
         if (h_pin) (void)hipHostFree(h_pin);
+        d_scol = nullptr;
+        d_srows = nullptr;
+        d_slv = nullptr;
+        d_srounds = nullptr;
+        streamOk = false;
         d_pyr = nullptr;
         d_tiles = nullptr;
         nTiles = 0;
@@ -2542,11 +2877,233 @@ struct orb_extractor {
         HIP_TRY(hipMalloc(&d_cells, cl.size() * sizeof(CellGeom)));
         if (!rt.empty()) HIP_TRY(hipMemcpy(d_rtab, rt.data(), rt.size() * 4, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(d_cells, cl.data(), cl.size() * sizeof(CellGeom), hipMemcpyHostToDevice));
+        if (int r = build_stream_plan(G, rt)) return r;
         g = G;
         cells = std::move(cl);
         rtab = std::move(rt);
         W = w0;
         H = h0;
+        return ORB_OK;
+    }
+
+    // k_pyr_stream's plan: the round schedule (greedy: level l computes every row whose source
+    // rows of level l-1 are in its ring), the ring capacity of each level (max over rounds of
+    // newest row written - oldest row read + 1), ring slots, per-row and per-quad tables.  K0
+    // (level-0 rows per round) is the largest whose rings fit PS_LDS_TARGET.  Frames with a
+    // level under 17 px (multiple reflections) or rings that never fit keep the per-level path.
+    int build_stream_plan(const Geom& G, const std::vector<int>& rt) {
+        streamOk = false;
+        const int L = nlevels;
+        if (L < 2) return ORB_OK;
+        for (int l = 0; l < L; ++l)
+            if (G.lv[l].w < 17 || G.lv[l].h < 17) return ORB_OK;
+        const int u0 = (G.lv[0].w + 15) / 16;
+        std::vector<std::vector<int>> s0(L), s1(L);
+        for (int l = 1; l < L; ++l) {
+            const LevelGeom& lg = G.lv[l];
+            const int hs = G.lv[l - 1].h;
+            const int* yofs = rt.data() + lg.rtab + 2 * lg.w;
+            s0[l].resize(lg.h);
+            s1[l].resize(lg.h);
+            for (int dy = 0; dy < lg.h; ++dy) {
+                s0[l][dy] = std::min(std::max(yofs[dy], 0), hs - 1);
+                s1[l][dy] = std::min(std::max(yofs[dy] + 1, 0), hs - 1);
+            }
+        }
+        auto ringPitch = [&](int l) { return (G.lv[l].w + 15) & ~15; };
+        auto nqOf = [&](int l) { return l == 0 ? G.lv[0].pitch / 16 : G.lv[l].pitch / 4; };
+        // column words (LDS-resident): one u32 per padded column of levels >= 1
+        // sx | a1 << 12 | (a0 - 2047 + a1) << 24 | simd << 26 | live << 27
+        std::vector<uint32_t> cw;
+        std::vector<int> colQuad(L, 0);
+        for (int l = 1; l < L; ++l) {
+            const LevelGeom& lg = G.lv[l];
+            const int* xofs = rt.data() + lg.rtab;
+            const int* alpha = xofs + lg.w;
+            colQuad[l] = (int)(cw.size() / 4);
+            for (int px = 0; px < 4 * nqOf(l); ++px) {
+                const int lx = orbdev::reflect101(std::min(px, lg.w + 2 * orbdev::EDGE - 1) - orbdev::EDGE, lg.w);
+                const int sx = xofs[lx];
+                const int a0 = lx < lg.xmax ? (alpha[lx] & 0xFFFF) : 2048;
+                const int a1 = lx < lg.xmax ? ((alpha[lx] >> 16) & 0xFFFF) : 0;
+                const int d = a0 - 2047 + a1;
+                if (sx < 0 || sx > 0xFFF || a1 > 0xFFF || d < 0 || d > 3) return ORB_OK;  // not encodable
+                uint32_t c = (uint32_t)sx | ((uint32_t)a1 << 12) | ((uint32_t)d << 24);
+                if (lx < lg.xs_resize) c |= 1u << 26;
+                if (px < lg.w + 2 * orbdev::EDGE) c |= 1u << 27;
+                cw.push_back(c);
+            }
+        }
+        const size_t colBytes = (cw.size() * 4 + 15) & ~(size_t)15;
+        std::vector<uint32_t> rounds;
+        std::vector<int> cap;
+        std::vector<std::vector<int>> plan;  // per round: lo, cnt per level
+        int K0 = 0, maxEnt = 0;
+        size_t lds = 0;
+        for (int k0 : {32, 24, 16, 12, 8, 6, 4, 2}) {
+            if (k0 * u0 > PS_NPF * 64 * PS_LOADERS) continue;
+            std::vector<int> next(L, 0), cp(L, 0);
+            std::vector<std::vector<int>> pl;
+            int me = 0;
+            bool ok = true;
+            for (int n = 0;; ++n) {
+                bool done = true;
+                for (int l = 0; l < L; ++l) done = done && next[l] >= G.lv[l].h;
+                if (done) break;
+                if (n > 65536) {
+                    ok = false;
+                    break;
+                }
+                std::vector<int> lo(L), cnt(L);
+                lo[0] = next[0];
+                cnt[0] = std::min(k0, G.lv[0].h - next[0]);
+                const int avail0 = next[0] + cnt[0];
+                for (int l = 1; l < L; ++l) {
+                    const int srcAvail = l == 1 ? avail0 : next[l - 1];
+                    int d = next[l];
+                    while (d < G.lv[l].h && s1[l][d] < srcAvail) ++d;
+                    lo[l] = next[l];
+                    cnt[l] = d - next[l];
+                }
+                for (int l = 0; l + 1 < L; ++l) {
+                    // level 0: the loaders store round n+1's rows during round n
+                    const int newest = (l == 0 ? std::min(avail0 + k0, G.lv[0].h) : next[l] + cnt[l]) - 1;
+                    int oldest = INT32_MAX;
+                    if (l == 0 && cnt[0]) oldest = lo[0];
+                    if (cnt[l + 1]) oldest = std::min(oldest, s0[l + 1][lo[l + 1]]);
+                    if (oldest != INT32_MAX) cp[l] = std::max(cp[l], newest - oldest + 1);
+                }
+                std::vector<int> rec(2 * L);
+                int ent = 0;
+                for (int l = 0; l < L; ++l) {
+                    rec[2 * l] = lo[l];
+                    rec[2 * l + 1] = cnt[l];
+                    ent += cnt[l];
+                    next[l] += cnt[l];
+                }
+                me = std::max(me, ent);
+                pl.push_back(std::move(rec));
+            }
+            if (!ok || me > PS_NPF * 64 * PS_LOADERS) continue;
+            size_t bytes = 0;
+            bool capOk = true;
+            for (int l = 0; l + 1 < L; ++l) {
+                cp[l] = std::min(std::max(cp[l], 1), G.lv[l].h);
+                capOk = capOk && cp[l] <= 255;
+                bytes += (size_t)cp[l] * ringPitch(l);
+            }
+            const int stride8 = (me + 1) & ~1;
+            bytes += colBytes + (size_t)2 * stride8 * 8;
+            if (capOk && bytes <= PS_LDS_TARGET) {
+                K0 = k0;
+                plan = std::move(pl);
+                cap = std::move(cp);
+                maxEnt = stride8;
+                lds = bytes;
+                break;
+            }
+        }
+        if (!K0) return ORB_OK;
+        std::vector<StreamLevel> lv(L);
+        int ringOff = 0;
+        for (int l = 0; l < L; ++l) {
+            const LevelGeom& lg = G.lv[l];
+            StreamLevel& s = lv[l];
+            s.nq = nqOf(l);
+            s.nqm = (uint32_t)((0x100000000ull + s.nq - 1) / (uint64_t)s.nq);
+            s.ringPitch = ringPitch(l);
+            s.ringOff = l + 1 < L ? ringOff : 0;
+            if (l + 1 < L) ringOff += cap[l] * s.ringPitch;
+            s.w = lg.w;
+            s.h = lg.h;
+            s.pitch = lg.pitch;
+            s.base = lg.base;
+            s.fstride = lg.fstride;
+        }
+        // waves per level: one each, then greedily to the level with the most work per wave
+        // (level-0 units are copies: weighted 1/4), up to one wave per 64 column units
+        if (L > PS_THREADS / 64 - PS_LOADERS) return ORB_OK;
+        {
+            std::vector<int> nw(L, 1);
+            for (int left = PS_THREADS / 64 - PS_LOADERS - L; left > 0; --left) {
+                int best = -1;
+                double bw = 0;
+                for (int l = 0; l < L; ++l) {
+                    if (nw[l] * 64 >= lv[l].nq) continue;
+                    const double wk = (double)lv[l].nq * G.lv[l].h * (l == 0 ? 0.25 : 1.0) / nw[l];
+                    if (wk > bw) {
+                        bw = wk;
+                        best = l;
+                    }
+                }
+                if (best < 0) break;
+                ++nw[best];
+            }
+            int ws = PS_LOADERS;
+            for (int l = 0; l < L; ++l) {
+                lv[l].waveStart = ws;
+                lv[l].nWaves = nw[l];
+                ws += nw[l];
+            }
+        }
+        const int colOff = ringOff;  // multiple of 16
+        for (int l = 1; l < L; ++l) lv[l].colOff = colOff + 16 * colQuad[l];
+        lv[0].colOff = 0;
+        // rounds (L level words + the first entry) and the row entries in round order
+        std::vector<uint2> ent;
+        for (const auto& rec : plan) {
+            int ne = 0;
+            for (int l = 0; l < L; ++l) {
+                if (rec[2 * l] > 0xFFF || rec[2 * l + 1] > 0x3F || ne > 0x3FFF) return ORB_OK;
+                rounds.push_back((uint32_t)rec[2 * l] | ((uint32_t)rec[2 * l + 1] << 12) | ((uint32_t)ne << 18));
+                ne += rec[2 * l + 1];
+            }
+            rounds.push_back((uint32_t)ent.size());
+            rounds.push_back((uint32_t)ne);
+            for (int l = 0; l < L; ++l)
+                for (int dy = rec[2 * l]; dy < rec[2 * l] + rec[2 * l + 1]; ++dy) {
+                    const uint32_t own = l + 1 < L ? (uint32_t)(dy % cap[l]) : 0xFFFFu;
+                    if (l == 0) {
+                        ent.push_back(make_uint2(own << 16, 0u));
+                    } else {
+                        const int cs = cap[l - 1];
+                        const uint32_t beta = (uint32_t)rt[G.lv[l].rtab + 2 * G.lv[l].w + G.lv[l].h + dy];
+                        ent.push_back(make_uint2((uint32_t)(s0[l][dy] % cs) | ((uint32_t)(s1[l][dy] % cs) << 8) | (own << 16),
+                                                 beta));
+                    }
+                }
+        }
+        // the magic divisions are exact over every task index of every round
+        for (int l = 0; l < L; ++l) {
+            int maxCnt = 0;
+            for (const auto& rec : plan) maxCnt = std::max(maxCnt, rec[2 * l + 1]);
+            for (uint32_t i = 0; i < (uint32_t)(maxCnt * lv[l].nq); ++i)
+                if ((uint32_t)(((uint64_t)i * lv[l].nqm) >> 32) != i / (uint32_t)lv[l].nq) return ORB_OK;
+        }
+        StreamGeom sg{};
+        sg.L = L;
+        sg.nRounds = (int)plan.size();
+        sg.u0 = u0;
+        sg.u0m = (uint32_t)((0x100000000ull + u0 - 1) / (uint64_t)u0);
+        for (uint32_t i = 0; i < (uint32_t)(K0 * u0); ++i)
+            if ((uint32_t)(((uint64_t)i * sg.u0m) >> 32) != i / (uint32_t)u0) return ORB_OK;
+        sg.colWords = (int)cw.size();
+        sg.colOff = colOff;
+        sg.rowOff = colOff + (int)colBytes;
+        sg.rowStride = maxEnt;
+        sg.cap0 = cap[0];
+        HIP_TRY(hipMalloc(&d_scol, std::max<size_t>(cw.size(), 1) * 4));
+        HIP_TRY(hipMemcpy(d_scol, cw.data(), cw.size() * 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMalloc(&d_srows, ent.size() * sizeof(uint2)));
+        HIP_TRY(hipMemcpy(d_srows, ent.data(), ent.size() * sizeof(uint2), hipMemcpyHostToDevice));
+        HIP_TRY(hipMalloc(&d_slv, L * sizeof(StreamLevel)));
+        HIP_TRY(hipMemcpy(d_slv, lv.data(), L * sizeof(StreamLevel), hipMemcpyHostToDevice));
+        HIP_TRY(hipMalloc(&d_srounds, rounds.size() * 4));
+        HIP_TRY(hipMemcpy(d_srounds, rounds.data(), rounds.size() * 4, hipMemcpyHostToDevice));
+        sgeom = sg;
+        streamLds = lds;
+        streamK0 = K0;
+        streamOk = true;
         return ORB_OK;
     }
 
@@ -2676,7 +3233,18 @@ struct orb_extractor {
             int r = profile_collect();
             if (r) return r;
         }
-        if (phases & 1u) {
+        if ((phases & 1u) && cn == 1 && streamOk && (B >= KR_STREAM_BATCH || pyrStreamAlways) && !pyrLegacy) {
+            // the whole pyramid in one streaming pass per frame (stage 0; stage 1 is empty)
+            stage_begin(0, st);
+            StreamGeom sg = sgeom;
+            const uintptr_t al = (uintptr_t)d_imgs | (uintptr_t)stride | (uintptr_t)fpitch;
+            sg.align = (al & 15u) == 0 ? 16 : (al & 3u) == 0 ? 4 : 1;
+            hipLaunchKernelGGL(k_pyr_stream, dim3(B), dim3(PS_THREADS), streamLds, st, d_imgs, stride, fpitch, d_pyr,
+                               (const uint32_t*)d_scol, (const uint2*)d_srows, (const StreamLevel*)d_slv,
+                               (const uint32_t*)d_srounds, sg);
+            stage_end(0, st);
+            pyrBatch = B;
+        } else if (phases & 1u) {
         stage_begin(0, st);
         {
             const LevelGeom& lg = g.lv[0];
@@ -2820,6 +3388,7 @@ int orb_extractor_create(int nfeatures, float scale_factor, int nlevels, int sco
     hipFuncSetAttribute((const void*)k_select<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
     hipFuncSetAttribute((const void*)k_rerun, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
     hipFuncSetAttribute((const void*)k_pyr_resize_tail, hipFuncAttributeMaxDynamicSharedMemorySize, RT_LDS_MAX);
+    hipFuncSetAttribute((const void*)k_pyr_stream, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
     orb_extractor* h = new orb_extractor();
     h->nfeatures = nfeatures;
     h->scaleFactor = scale_factor;
@@ -3146,6 +3715,22 @@ int orb_profile_enable(orb_extractor_t* h, int enable) {
     return orb_profile_enable_stages(h, enable ? (1u << orb_extractor::kStages) - 1u : 0u);
 }
 
+int orb_debug_set_pyramid_path(orb_extractor_t* h, int mode) {
+    if (!h || mode < 0 || mode > 2) return set_err(ORB_EINVAL, "mode must be 0, 1 or 2");
+    h->pyrLegacy = mode == 1;
+    h->pyrStreamAlways = mode == 2;
+    return ORB_OK;
+}
+
+int orb_debug_pyramid_plan(const orb_extractor_t* h, int* rows_per_round, int* rounds, int* lds_bytes) {
+    if (!h) return set_err(ORB_EINVAL, "bad handle");
+    if (!h->streamOk) return 0;
+    if (rows_per_round) *rows_per_round = h->streamK0;
+    if (rounds) *rounds = h->sgeom.nRounds;
+    if (lds_bytes) *lds_bytes = (int)h->streamLds;
+    return 1;
+}
+
 int orb_extract_set_phases(orb_extractor_t* h, unsigned phase_mask) {
     if (!h) return set_err(ORB_EINVAL, "bad handle");
     if (phase_mask == 0u || (phase_mask & ~3u)) return set_err(ORB_EINVAL, "phase_mask must be 1, 2 or 3");
@@ -3257,6 +3842,15 @@ int orb_debug_blur_image(orb_extractor_t* h, int b, int l, uint8_t* out) {
     return ORB_OK;
 }
 
+#if PS_TIMING
+extern "C" int orb_debug_ps_timing(unsigned long long* out6) {
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out6, HIP_SYMBOL(g_pstime), 32 * sizeof(unsigned long long)));
+    unsigned long long z[32] = {};
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_pstime), z, sizeof(z)));
+    return ORB_OK;
+}
+#endif
 // Per-cell FAST counts (after fallback) of frame `b`, level `l`, row-major cells.
 #if KF_TIMING
 // experiment builds: k_fast's per-phase s_memtime sums {stage, rows, drain, barrier, nms, waves}

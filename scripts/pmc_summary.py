@@ -20,7 +20,7 @@ import json
 from collections import defaultdict
 
 
-WIDE_LOADS = {"k_pyr0", "k_pyr_resize", "k_fast", "k_orient_desc"}
+WIDE_LOADS = {"k_pyr0", "k_pyr_stream", "k_pyr_resize", "k_fast", "k_orient_desc"}
 
 
 def main():
@@ -43,10 +43,13 @@ def main():
     mean = {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in acc.items()
             if not k.startswith("__amd") and "elementwise" not in k and "at::" not in k}
     known = a.batch * a.width * a.height
-    cal = known / (mean["k_pyr0"]["FETCH_SIZE"] * 1024.0) if "k_pyr0" in mean else None
+    # the kernel that reads exactly the B input frames from HBM: k_pyr0, or k_pyr_stream (whose
+    # other reads, the shared column / row tables, are L2-resident)
+    ck = "k_pyr0" if "k_pyr0" in mean else "k_pyr_stream"
+    cal = known / (mean[ck]["FETCH_SIZE"] * 1024.0) if ck in mean else None
     out = {"source": a.root.rstrip("/").split("/")[-1],
            "workload": {"width": a.width, "height": a.height, "batch": a.batch, "nfeatures": a.nfeatures},
-           "read_calibration": {"kernel": "k_pyr0", "known_read_bytes": known, "factor": cal,
+           "read_calibration": {"kernel": ck, "known_read_bytes": known, "factor": cal,
                                 "applies_to": sorted(WIDE_LOADS), "dword_factor": a.dword_factor,
                                 "dword_factor_source": "r01_v16_pmc (k_pyr0 with dword loads)"},
            "per_launch": {}}
@@ -61,7 +64,7 @@ def main():
                                 "write_bytes": wr, "hbm_bytes": rd + wr,
                                 **{c: v for c, v in d.items() if c.startswith("SQ_")}}
         print(f"{k:16s} read {rd / 1e6:10.2f} MB  write {wr / 1e6:10.2f} MB  per launch")
-    print(f"read calibration factor (k_pyr0): {cal}")
+    print(f"read calibration factor ({ck}): {cal}")
     if a.json:
         json.dump(out, open(a.json, "w"), indent=1)
 
