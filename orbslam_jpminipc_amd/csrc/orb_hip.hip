@@ -621,12 +621,11 @@ __device__ unsigned long long g_pstime[32];
 #endif
 __global__ void __launch_bounds__(PS_THREADS) __attribute__((amdgpu_waves_per_eu(PS_WAVES)))
 k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uint8_t* __restrict__ pyr,
-             const uint32_t* __restrict__ colWords, const uint2* __restrict__ rowEntries,
+             const uint32_t* __restrict__ colWords, const uint4* __restrict__ rowEntries,
              const StreamLevel* __restrict__ slv, const uint32_t* __restrict__ rounds, StreamGeom sg) {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_ring[];
     const int b = blockIdx.x, tid = threadIdx.x;
     const int rw = sg.L + 2;  // words per round record
-    uint2* stage = (uint2*)(s_ring + sg.rowOff);
     for (int i = tid; i < sg.colWords; i += PS_THREADS) ((uint32_t*)(s_ring + sg.colOff))[i] = colWords[i];
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     // The first PS_LOADERS waves are loaders: during round n they bring the level-0 rows and
@@ -640,7 +639,6 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
             if (n < sg.nRounds) {
                 const uint32_t e = rounds[n * rw];
                 const int lo = e & 0xFFF, units = (int)((e >> 12) & 0x3F) * sg.u0;
-                const int eFirst = rounds[n * rw + sg.L], ne = rounds[n * rw + sg.L + 1];
                 for (int i0 = tid; i0 < units; i0 += PS_LB * 64 * PS_LOADERS) {
                     uint4 pf[PS_LB];
 #pragma unroll
@@ -660,7 +658,6 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
                         }
                     }
                 }
-                for (int i = tid; i < ne; i += 64 * PS_LOADERS) stage[(n & 1) * sg.rowStride + i] = rowEntries[eFirst + i];
             }
             lds_barrier();  // round n's data is in LDS (n = 0: before the first round)
         }
@@ -672,12 +669,9 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
         if (wave >= slv[l].waveStart && wave < slv[l].waveStart + slv[l].nWaves) myL = l;
     const int ws = slv[myL].waveStart, nWaves = slv[myL].nWaves;
     const bool idle = wave < ws || wave >= ws + nWaves;  // a wave no level needed
-    const int nq = slv[myL].nq, w = slv[myL].w, h = slv[myL].h, pitch = slv[myL].pitch;
-    const int ownOff = slv[myL].ringOff, ownPitch = slv[myL].ringPitch, colOff = slv[myL].colOff;
-    const int srcOff = slv[myL > 0 ? myL - 1 : 0].ringOff, srcPitch = slv[myL > 0 ? myL - 1 : 0].ringPitch;
+    const int nq = slv[myL].nq, w = slv[myL].w, colOff = slv[myL].colOff;
     uint8_t* D = pyr + slv[myL].base + (long long)b * slv[myL].fstride;
     const int ql = (wave - ws) * 64 + lane, qs = 64 * nWaves;
-    const int mirBot = h - 17;  // rows >= mirBot (and <= h-2) have a bottom mirror
     lds_barrier();
 #if PS_TIMING
     unsigned long long acc[5] = {0, 0, 0, 0, 0};
@@ -685,18 +679,19 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
     for (int n = 0; n < sg.nRounds; ++n) {
         PS_T(t1);
         const uint32_t e = idle ? 0u : rounds[n * rw + myL];
-        const int lo = e & 0xFFF, cnt = PS_EXP == 1 ? 0 : (e >> 12) & 0x3F;
-        const uint2* E = stage + (n & 1) * sg.rowStride + (e >> 18);
+        const int cnt = PS_EXP == 1 ? 0 : (e >> 12) & 0x3F;
+        // the level's row entries of this round (scalar loads: lgkmcnt, never behind stores):
+        // {source row 0, source row 1 (LDS addresses), b0 << 12, b1 << 12, own ring row (LDS
+        //  address, ~0u: none), padded-row offset, top mirror offset, bottom mirror offset (~0u: none)}
+        const uint4* E = rowEntries + 2 * ((int)rounds[n * rw + sg.L] + (int)(e >> 18));
         if (cnt > 0 && myL == 0) {
             // padded level-0 rows from the ring (k_pyr0's copyMakeBorder), 16 B per unit
             for (int c = ql; c < nq; c += qs) {
                 const int px = 16 * c;
                 const bool inner = px >= EDGE && px <= w;
-                uint8_t* Dc = D + px;
                 for (int k = 0; k < cnt; ++k) {
-                    const int r = lo + k;
-                    const int slot = __builtin_amdgcn_readfirstlane((int)(E[k].x >> 16));
-                    const uint8_t* R = s_ring + ownOff + slot * ownPitch;
+                    const uint4 e0 = E[2 * k], e1 = E[2 * k + 1];
+                    const uint8_t* R = s_ring + e0.x;
                     uint4 v;
                     if (inner) {
                         v = *(const uint4*)(R + px - EDGE);
@@ -719,12 +714,12 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
                         v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
                     }
                     if (PS_EXP == 2) {
-                        if (v.x == 0x12345678u) *(uint4*)Dc = v;
+                        if (v.x == 0x12345678u) *(uint4*)(D + px) = v;
                         continue;
                     }
-                    *(uint4*)(Dc + __mul24(r + EDGE, pitch)) = v;
-                    if (r >= 1 && r <= EDGE) *(uint4*)(Dc + __mul24(EDGE - r, pitch)) = v;
-                    if (r >= mirBot && r <= h - 2) *(uint4*)(Dc + __mul24(2 * h + 14 - r, pitch)) = v;
+                    *(uint4*)(D + e1.y + px) = v;
+                    if (e1.z != 0xFFFFFFFFu) *(uint4*)(D + e1.z + px) = v;
+                    if (e1.w != 0xFFFFFFFFu) *(uint4*)(D + e1.w + px) = v;
                 }
             }
         } else if (cnt > 0) {
@@ -745,12 +740,12 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
                     if (cc[j] & (1u << 27)) live |= 0xFFu << (8 * j);
                 }
                 const bool allSimd = simd == 0xFu;
-                // HResizeLinear of source row `slot`: H = S[sx] a0 + S[sx+1] a1 (a1 == 0 where
-                // OpenCV reads S[sx] only: the byte after it is multiplied by 0; it lies in the
-                // ring row's slack or the next LDS row, never outside the allocation).  On
-                // all-SSE2 quads h keeps (H >> 4) << 8 for the v_mul_hi_u32_u24 below.
-                auto hrow = [&](int slot, uint32_t* hh) {
-                    const uint8_t* R = s_ring + srcOff + slot * srcPitch;
+                // HResizeLinear of the source row at LDS address `ra`: H = S[sx] a0 + S[sx+1] a1
+                // (a1 == 0 where OpenCV reads S[sx] only: the byte after it is multiplied by 0; it
+                // lies in the ring row's slack or the next LDS row, never outside the allocation).
+                // On all-SSE2 quads h keeps (H >> 4) << 4 = H & ~15 for the v_mul_hi_u32_u24 below.
+                auto hrow = [&](uint32_t ra, uint32_t* hh) {
+                    const uint8_t* R = s_ring + ra;
                     uint32_t lo8[4], hi8[4];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
@@ -761,20 +756,16 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
                     for (int j = 0; j < 4; ++j) {
                         const uint32_t H = __builtin_amdgcn_udot2(__builtin_bit_cast(ps_u16x2, lo8[j] | (hi8[j] << 16)),
                                                                   __builtin_bit_cast(ps_u16x2, ap[j]), 0u, false);
-                        hh[j] = allSimd ? ((H << 4) & 0xFFFFFF00u) : H;
+                        hh[j] = allSimd ? (H & 0xFFFFFFF0u) : H;
                     }
                 };
                 const int cx = 4 * q - EDGE;
                 const bool roi = cx >= 0 && cx < w;
-                uint8_t* Dc = D + 4 * q;
-                int sA = -1, sB = -1;
+                uint32_t sA = 0xFFFFFFFFu, sB = 0xFFFFFFFFu;
                 uint32_t hA[4] = {0u, 0u, 0u, 0u}, hB[4] = {0u, 0u, 0u, 0u};
                 for (int k = 0; k < cnt; ++k) {
-                    const int dy = lo + k;
-                    // entry (wave-uniform): slot0 | slot1 << 8 | own << 16 (0xFFFF: none), beta
-                    const uint2 en0 = E[k];
-                    const uint32_t ex = __builtin_amdgcn_readfirstlane(en0.x), ey = __builtin_amdgcn_readfirstlane(en0.y);
-                    const int s0 = (int)(ex & 0xFFu), s1 = (int)((ex >> 8) & 0xFFu);
+                    const uint4 e0 = E[2 * k], e1 = E[2 * k + 1];
+                    const uint32_t s0 = e0.x, s1 = e0.y;
                     if (s0 != sA) {
                         if (s0 == sB) {
 #pragma unroll
@@ -793,16 +784,15 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
                         }
                         sB = s1;
                     }
-                    const uint32_t b0 = ey & 0xFFFFu, b1 = ey >> 16;
                     uint32_t word = 0;
                     if (allSimd) {
                         // VResizeLinearVec_32s8u: ((H >> 4) * b) >> 16 per term = the high 32 bits of
-                        // ((H >> 4) << 8) * (b << 8) (both < 2^24), + 2 >> 2
-                        const uint32_t B0 = b0 << 8, B1 = b1 << 8;
+                        // (H & ~15) * (b << 12) (both < 2^24), + 2 >> 2
 #pragma unroll
                         for (int j = 0; j < 4; ++j)
-                            word |= ((mulhi24(hA[j], B0) + mulhi24(hB[j], B1) + 2u) >> 2) << (8 * j);
+                            word |= ((mulhi24(hA[j], e0.z) + mulhi24(hB[j], e0.w) + 2u) >> 2) << (8 * j);
                     } else {
+                        const uint32_t b0 = e0.z >> 12, b1 = e0.w >> 12;
 #pragma unroll
                         for (int j = 0; j < 4; ++j) {
                             const uint32_t r = ((simd >> j) & 1u)
@@ -813,14 +803,13 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
                     }
                     word &= live;
                     if (PS_EXP != 2) {
-                        *(uint32_t*)(Dc + __mul24(dy + EDGE, pitch)) = word;
-                        if (dy >= 1 && dy <= EDGE) *(uint32_t*)(Dc + __mul24(EDGE - dy, pitch)) = word;
-                        if (dy >= mirBot && dy <= h - 2) *(uint32_t*)(Dc + __mul24(2 * h + 14 - dy, pitch)) = word;
+                        *(uint32_t*)(D + e1.y + 4 * q) = word;
+                        if (e1.z != 0xFFFFFFFFu) *(uint32_t*)(D + e1.z + 4 * q) = word;
+                        if (e1.w != 0xFFFFFFFFu) *(uint32_t*)(D + e1.w + 4 * q) = word;
                     } else if (word == 0x12345678u) {
-                        *(uint32_t*)Dc = word;
+                        *(uint32_t*)(D + 4 * q) = word;
                     }
-                    const int own = (int)(ex >> 16);
-                    if (own != 0xFFFF && roi) *(uint32_t*)(s_ring + ownOff + __mul24(own, ownPitch) + cx) = word;
+                    if (e1.x != 0xFFFFFFFFu && roi) *(uint32_t*)(s_ring + e1.x + cx) = word;
                 }
             }
         }
@@ -2488,7 +2477,7 @@ struct orb_extractor {
     size_t streamLds = 0;
     int streamK0 = 0;
     uint32_t* d_scol = nullptr;
-    uint2* d_srows = nullptr;
+    uint4* d_srows = nullptr;
     StreamLevel* d_slv = nullptr;
     uint32_t* d_srounds = nullptr;
     // device workspace
@@ -2993,7 +2982,7 @@ struct orb_extractor {
                 bytes += (size_t)cp[l] * ringPitch(l);
             }
             const int stride8 = (me + 1) & ~1;
-            bytes += colBytes + (size_t)2 * stride8 * 8;
+            bytes += colBytes;
             if (capOk && bytes <= PS_LDS_TARGET) {
                 K0 = k0;
                 plan = std::move(pl);
@@ -3049,8 +3038,10 @@ struct orb_extractor {
         const int colOff = ringOff;  // multiple of 16
         for (int l = 1; l < L; ++l) lv[l].colOff = colOff + 16 * colQuad[l];
         lv[0].colOff = 0;
-        // rounds (L level words + the first entry) and the row entries in round order
-        std::vector<uint2> ent;
+        // rounds (L level words + the first entry) and the row entries in round order: per row
+        // {source row 0, source row 1 (LDS addresses), b0 << 12, b1 << 12, own ring row (LDS
+        //  address or ~0u), padded-row offset, top mirror offset, bottom mirror offset (~0u: none)}
+        std::vector<uint32_t> ent;
         for (const auto& rec : plan) {
             int ne = 0;
             for (int l = 0; l < L; ++l) {
@@ -3058,18 +3049,24 @@ struct orb_extractor {
                 rounds.push_back((uint32_t)rec[2 * l] | ((uint32_t)rec[2 * l + 1] << 12) | ((uint32_t)ne << 18));
                 ne += rec[2 * l + 1];
             }
-            rounds.push_back((uint32_t)ent.size());
+            rounds.push_back((uint32_t)(ent.size() / 8));
             rounds.push_back((uint32_t)ne);
             for (int l = 0; l < L; ++l)
                 for (int dy = rec[2 * l]; dy < rec[2 * l] + rec[2 * l + 1]; ++dy) {
-                    const uint32_t own = l + 1 < L ? (uint32_t)(dy % cap[l]) : 0xFFFFu;
+                    const LevelGeom& lg = G.lv[l];
+                    const uint32_t own =
+                        l + 1 < L ? (uint32_t)(lv[l].ringOff + (dy % cap[l]) * lv[l].ringPitch) : 0xFFFFFFFFu;
+                    const uint32_t main = (uint32_t)((dy + orbdev::EDGE) * lg.pitch);
+                    const uint32_t top = dy >= 1 && dy <= orbdev::EDGE ? (uint32_t)((orbdev::EDGE - dy) * lg.pitch) : 0xFFFFFFFFu;
+                    const uint32_t bot = dy >= lg.h - 17 && dy <= lg.h - 2 ? (uint32_t)((2 * lg.h + 14 - dy) * lg.pitch) : 0xFFFFFFFFu;
                     if (l == 0) {
-                        ent.push_back(make_uint2(own << 16, 0u));
+                        ent.insert(ent.end(), {own, 0u, 0u, 0u, 0xFFFFFFFFu, main, top, bot});
                     } else {
                         const int cs = cap[l - 1];
-                        const uint32_t beta = (uint32_t)rt[G.lv[l].rtab + 2 * G.lv[l].w + G.lv[l].h + dy];
-                        ent.push_back(make_uint2((uint32_t)(s0[l][dy] % cs) | ((uint32_t)(s1[l][dy] % cs) << 8) | (own << 16),
-                                                 beta));
+                        const uint32_t beta = (uint32_t)rt[lg.rtab + 2 * lg.w + lg.h + dy];
+                        const uint32_t a0 = (uint32_t)(lv[l - 1].ringOff + (s0[l][dy] % cs) * lv[l - 1].ringPitch);
+                        const uint32_t a1 = (uint32_t)(lv[l - 1].ringOff + (s1[l][dy] % cs) * lv[l - 1].ringPitch);
+                        ent.insert(ent.end(), {a0, a1, (beta & 0xFFFFu) << 12, (beta >> 16) << 12, own, main, top, bot});
                     }
                 }
         }
@@ -3094,8 +3091,8 @@ struct orb_extractor {
         sg.cap0 = cap[0];
         HIP_TRY(hipMalloc(&d_scol, std::max<size_t>(cw.size(), 1) * 4));
         HIP_TRY(hipMemcpy(d_scol, cw.data(), cw.size() * 4, hipMemcpyHostToDevice));
-        HIP_TRY(hipMalloc(&d_srows, ent.size() * sizeof(uint2)));
-        HIP_TRY(hipMemcpy(d_srows, ent.data(), ent.size() * sizeof(uint2), hipMemcpyHostToDevice));
+        HIP_TRY(hipMalloc(&d_srows, ent.size() * 4));
+        HIP_TRY(hipMemcpy(d_srows, ent.data(), ent.size() * 4, hipMemcpyHostToDevice));
         HIP_TRY(hipMalloc(&d_slv, L * sizeof(StreamLevel)));
         HIP_TRY(hipMemcpy(d_slv, lv.data(), L * sizeof(StreamLevel), hipMemcpyHostToDevice));
         HIP_TRY(hipMalloc(&d_srounds, rounds.size() * 4));
@@ -3240,7 +3237,7 @@ struct orb_extractor {
             const uintptr_t al = (uintptr_t)d_imgs | (uintptr_t)stride | (uintptr_t)fpitch;
             sg.align = (al & 15u) == 0 ? 16 : (al & 3u) == 0 ? 4 : 1;
             hipLaunchKernelGGL(k_pyr_stream, dim3(B), dim3(PS_THREADS), streamLds, st, d_imgs, stride, fpitch, d_pyr,
-                               (const uint32_t*)d_scol, (const uint2*)d_srows, (const StreamLevel*)d_slv,
+                               (const uint32_t*)d_scol, (const uint4*)d_srows, (const StreamLevel*)d_slv,
                                (const uint32_t*)d_srounds, sg);
             stage_end(0, st);
             pyrBatch = B;
