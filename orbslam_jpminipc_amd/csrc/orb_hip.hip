@@ -574,7 +574,9 @@ struct StreamGeom {
 #ifndef KR_STREAM_BATCH  // smallest batch that uses k_pyr_stream (one workgroup per frame)
 #define KR_STREAM_BATCH 256
 #endif
+#ifndef PS_LDS_TARGET
 #define PS_LDS_TARGET (76 * 1024)  // two workgroups per CU
+#endif
 
 __device__ __forceinline__ uint4 load_unit16(const uint8_t* p, int nvalid, int align) {
     if (nvalid >= 16 && align == 16) return *(const uint4*)p;
@@ -876,9 +878,10 @@ __device__ __forceinline__ int fast_strength_packed(const uint8_t* p, int TP) {
 // Mat), survivors written in raster order as ((S - 1) << 24) | (y << 12) | x.  Returns the
 // survivor count (all threads).  smem: Sp (dwp x dh) | Fl (dwp x dh) | rowc | In, rerun_lds()
 // bytes.
+#define RR_Q 128  // per-wave queue of compass survivors (< 64 carried + 64 new), + a trash slot
 inline size_t rerun_lds(int dw, int dh) {
     const size_t dwp = (size_t)((dw + 3) & ~3), inW = (size_t)((3 + dw + 6 + 3) & ~3);
-    return 2 * dwp * dh + 4 * (size_t)((dh + 3) & ~3) + inW * (dh + 6) + 16;
+    return 2 * dwp * dh + 4 * (size_t)((dh + 3) & ~3) + inW * (dh + 6) + 16 + 2 * (8 + 4 * (RR_Q + 8));
 }
 __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int dw, int dh, int rx0, int ry0, int t,
                                uint8_t* smem, uint32_t* __restrict__ out, int tid) {
@@ -899,10 +902,50 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
         for (int i = tid; i < nw; i += 256) ((uint32_t*)Fl)[i] = 0u;
     }
     __syncthreads();
-    // the strength of every pixel (corner at t <=> S > t; the NMS below reads only S > t)
-    for (int i = tid; i < dh * dw; i += 256) {
-        const int yy = i / dw, xx = i - yy * dw;
-        Sp[yy * dwp + xx] = (uint8_t)max(fast_strength_packed(In + (yy + 3) * inW + xx + 3 + o, inW), 0);
+    // the strength plane (corner at t <=> S > t; the NMS below reads only S > t, so a pixel
+    // known not to be a corner may hold 0): per wave, 64 pixels at a time through the compass
+    // test of cv::FAST at t (a 9-arc always covers two cyclically adjacent points of {0, 4, 8,
+    // 12}: a necessary condition), survivors queued, the exact strength computed in full
+    // 64-lane passes from the top of the queue (LDS accesses of one wave complete in order)
+    {
+        uint16_t* q = (uint16_t*)(In + inW * (dh + 6)) + 8 + wave * (RR_Q + 8);  // after the staged ROI
+        const uint32_t m = (uint32_t)((0x100000000ull + dw - 1) / (uint64_t)dw);  // i / dw = umulhi(i, m)
+        const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+        const int total = dh * dw;
+        int np = 0;
+        auto pass = [&](int base, int n) {  // q[base .. base + n), n <= 64
+            if (lane < n) {
+                const int i = q[base + lane];
+                const int yy = (int)__umulhi((uint32_t)i, m), xx = i - yy * dw;
+                Sp[yy * dwp + xx] = (uint8_t)max(fast_strength_packed(In + (yy + 3) * inW + xx + 3 + o, inW), 0);
+            }
+        };
+        // one strength call site (the last round flushes the queue's remainder)
+        for (int i0 = wave * 64;; i0 += 256) {
+            const bool last = i0 >= total;  // wave-uniform
+            if (!last) {
+                const int i = i0 + lane;
+                bool c = false;
+                if (i < total) {
+                    const int yy = (int)__umulhi((uint32_t)i, m), xx = i - yy * dw;
+                    const uint8_t* p = In + (yy + 3) * inW + xx + 3 + o;
+                    const int v = p[0], q0 = p[3 * inW], q4 = p[3], q8 = p[-3 * inW], q12 = p[-3];
+                    c = min(max(q0, q8), max(q4, q12)) > v + t || max(min(q0, q8), min(q4, q12)) < v - t;
+                    Sp[yy * dwp + xx] = 0;
+                }
+                const uint64_t bm = __ballot(c);
+                q[c ? np + __popcll(bm & below) : RR_Q] = (uint16_t)i;  // RR_Q: trash slot
+                np += __popcll(bm);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            while (np >= 64 || (last && np > 0)) {
+                const int n = min(np, 64);
+                np -= n;
+                pass(np, n);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (last) break;
+        }
     }
     __syncthreads();
     // 3x3 NMS; each row's survivor count comes from the same ballots (no second pass)
@@ -991,7 +1034,7 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
 // Large batches keep the re-runs inside k_select<.., true>: there every CU is busy anyway.
 #define RERUN_FLAG 0x40000000
 #define COUNT_MASK 0x3FFFFFFF
-__global__ void __launch_bounds__(256) k_rerun(const uint8_t* __restrict__ pyr, uint32_t* __restrict__ cand,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_rerun(const uint8_t* __restrict__ pyr, uint32_t* __restrict__ cand,
                                                int* __restrict__ cellCount, Geom g,
                                                const CellGeom* __restrict__ cells, int NWG) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
