@@ -1168,7 +1168,8 @@ __device__ __forceinline__ int cell_of(const int* off, int n, int i) {
 #define KS_CELL_SPREAD 1
 #endif
 #ifndef KS_SEP_PIXELS
-#define KS_SEP_PIXELS 400000  // and frames larger than this
+#define KS_SEP_PIXELS 0  // and frames larger than this (0: every batch; the in-k_select re-run
+                         // path stays for experiments: -DKS_SEP_PIXELS=100000000)
 #endif
 #ifndef KS_WAVES
 #define KS_WAVES 2  // waves per SIMD the register allocation targets
@@ -3328,10 +3329,10 @@ struct orb_extractor {
         hipLaunchKernelGGL(k_fast, dim3(nTiles, B), dim3(256), 0, st, d_pyr, g, d_tiles, d_cand, d_cellCount);
         stage_end(2, st);
         stage_begin(3, st);
-        // FAST(7) re-runs: spread over NWG workgroups per level first (k_rerun) for a few frames
-        // and for large frames (whose re-runs are many and long); inside k_select (one workgroup
-        // per level and frame, no extra launch) otherwise.  Measured at B = 512: 640x480 0.27 ms
-        // inside vs 0.33 apart; 1241x376 0.79 vs 0.74; 1280x720 1.70 vs 1.36.
+        // FAST(7) re-runs: spread over NWG workgroups per level first (k_rerun), or inside
+        // k_select (one workgroup per level and frame, no extra launch).  With the compass
+        // pre-filtered re-run, apart is faster at every measured size (B = 512, re-run + select:
+        // 640x480 0.190 vs 0.239 ms inside; 1241x376 0.497 vs 0.696; 1280x720 0.864 vs 1.421).
         const bool sep = (B < KS_SEP_BATCH || (long long)W * H > KS_SEP_PIXELS) && cellLds;
         if (sep && !KS_SKIP_RERUN) {
             const int NWG = std::min(32, std::max(1, 512 / (B * nlevels)));
