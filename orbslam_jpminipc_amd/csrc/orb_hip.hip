@@ -2510,6 +2510,7 @@ struct orb_extractor {
     Geom g{};
     std::vector<CellGeom> cells;
     std::vector<int> rtab;
+    size_t listLds = 0;  // k_select<.., false> (re-runs in k_rerun): the survivor lists only
     size_t cellLds = 0, selectLds = 0;  // a FAST(7) re-run's LDS (largest cell); k_select's
     size_t resizeLds[ORB_MAX_LEVELS] = {}, resizeLdsS[ORB_MAX_LEVELS] = {};
     int resizeTail = 0;           // first level of k_pyr_resize_tail (nlevels: none)
@@ -2778,7 +2779,8 @@ struct orb_extractor {
             for (size_t i = lg.cell0; i < cl.size(); ++i) cl[i].candOff = cand + (int)(i - lg.cell0) * capMax;
             cand += (int)(cl.size() - lg.cell0) * capMax;
         }
-        selectLds = std::max(cellLds, (size_t)(scoreType == ORB_HARRIS_SCORE ? 4 : 2) * SELECT_CAP * 4);
+        listLds = (size_t)(scoreType == ORB_HARRIS_SCORE ? 4 : 2) * SELECT_CAP * 4;
+        selectLds = std::max(cellLds, listLds);
         if (selectLds > 150 * 1024) return set_err(ORB_ENOTSUP, "FAST cell larger than the LDS budget");
         // resize tables, l >= 1
         for (int l = 1; l < nlevels; ++l) {
@@ -3342,14 +3344,14 @@ struct orb_extractor {
         const dim3 sg(B, nlevels);
         if (scoreType == ORB_HARRIS_SCORE) {
             if (sep)
-                hipLaunchKernelGGL((k_select<true, false>), sg, dim3(256), selectLds, st, d_pyr, d_cand, d_cand2,
+                hipLaunchKernelGGL((k_select<true, false>), sg, dim3(256), listLds, st, d_pyr, d_cand, d_cand2,
                                    d_cellCount, g, d_cells, d_lvl, d_lvlCount, d_candH, d_lvlResp, harrisScale4);
             else
                 hipLaunchKernelGGL((k_select<true, true>), sg, dim3(256), selectLds, st, d_pyr, d_cand, d_cand2,
                                    d_cellCount, g, d_cells, d_lvl, d_lvlCount, d_candH, d_lvlResp, harrisScale4);
         } else {
             if (sep)
-                hipLaunchKernelGGL((k_select<false, false>), sg, dim3(256), selectLds, st, d_pyr, d_cand, d_cand2,
+                hipLaunchKernelGGL((k_select<false, false>), sg, dim3(256), listLds, st, d_pyr, d_cand, d_cand2,
                                    d_cellCount, g, d_cells, d_lvl, d_lvlCount, (uint64_t*)nullptr, (float*)nullptr, 0.f);
             else
                 hipLaunchKernelGGL((k_select<false, true>), sg, dim3(256), selectLds, st, d_pyr, d_cand, d_cand2,
