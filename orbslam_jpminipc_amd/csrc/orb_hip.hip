@@ -115,6 +115,7 @@ struct Geom {
     int nCells;        // cells per frame (all levels)
     int candPerFrame;  // candidate slots per frame (u32)
     int kpCap;         // keypoint slots per frame (sum of nDesired)
+    int selCap;        // k_select: survivors per level held in LDS (select_cap)
     int fastTh;        // clamped to [0, 255]
     int scoreType;
     int taps[4];       // Gaussian 7-tap fixed-point kernel, centre first: 55, 49, 34, 18
@@ -1085,12 +1086,18 @@ struct ScoreGreater {  // KeypointResponseGreater on the packed FAST score
 // retainBest's nth_element depends on; (3) nToRetain / redistribution (ORBextractor.cc:622-670);
 // (4) retainBest per cell, concatenation in cell order, retainBest to the level quota
 // (ORBextractor.cc:680-701) — exact libstdc++ nth_element replays.  Lists live in LDS when the
-// level's survivors fit (SELECT_CAP), otherwise in the frame's scratch area `cand2`.
+// level's survivors fit (Geom::selCap), otherwise in the frame's scratch area `cand2`.
 #ifndef SELECT_CAP
-#define SELECT_CAP 3072  // survivors per level held in LDS (a few hundred to ~2000 at every
-                         // BASELINE size; beyond: the global-scratch path).  24 KB lets 6
-                         // work-groups share a CU (6144: 3): KITTI 0.70 -> 0.55 ms, 720p 1.33 -> 1.20
+#define SELECT_CAP 0  // > 0: survivors per level held in LDS for every geometry (experiments)
 #endif
+// survivors per level held in LDS (beyond: the global-scratch path, same result), per frame
+// size: (W*H / 200) rounded down to 512 in [1024, 3072] -- 1536 at 640x480 (6 -> 10 work-groups
+// per CU: 0.177 -> 0.146 ms with 3072), 2048 at 1241x376 (0.499 -> 0.474), 3072 at 1280x720
+// (2048 there: 0.84 -> 1.14, most levels past LDS)
+inline int select_cap(int w, int h) {
+    if (SELECT_CAP > 0) return SELECT_CAP;
+    return std::min(3072, std::max(1024, (int)(((long long)w * h / 200) & ~511ll)));
+}
 // KeypointResponseGreater on HARRIS_SCORE elements: float response in the high word, the
 // packed FAST record (identity) in the low word.
 struct HarrisGreater {
@@ -1311,7 +1318,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
     }
     __syncthreads();
     const int M = s_off[nC];
-    constexpr int selCap = SELECT_CAP;
+    const int selCap = g.selCap;
     const bool inLds = M <= selCap;
     uint32_t* raw = (uint32_t*)smem;                                      // arrival order
     uint32_t* srt = inLds ? raw + selCap : cand2 + (long long)b * g.candPerFrame;  // raster order
@@ -2779,7 +2786,8 @@ struct orb_extractor {
             for (size_t i = lg.cell0; i < cl.size(); ++i) cl[i].candOff = cand + (int)(i - lg.cell0) * capMax;
             cand += (int)(cl.size() - lg.cell0) * capMax;
         }
-        listLds = (size_t)(scoreType == ORB_HARRIS_SCORE ? 4 : 2) * SELECT_CAP * 4;
+        G.selCap = select_cap(w0, h0);
+        listLds = (size_t)(scoreType == ORB_HARRIS_SCORE ? 4 : 2) * G.selCap * 4;
         selectLds = std::max(cellLds, listLds);
         if (selectLds > 150 * 1024) return set_err(ORB_ENOTSUP, "FAST cell larger than the LDS budget");
         // resize tables, l >= 1
