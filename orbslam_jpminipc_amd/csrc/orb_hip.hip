@@ -143,7 +143,7 @@ __constant__ float c_patternf[1024];  // the same pattern as floats: lane l's 8 
 // IC_Angle disc masks (ORBextractor.cc:124-151 with umax, 495-510) of the 31 x 9 patch dwords for
 // each byte alignment sh of the patch in its dword row: byte i of dword n = 9 r + c is inside the
 // disc iff |4c + i - sh - 15| <= umax[|r - 15|]
-__constant__ uint32_t c_icmask[4 * 288];
+__constant__ uint32_t c_icmask[4 * 320];  // 279 patch dwords per alignment, zero-padded to 5 x 64
 // ---- pyramid --------------------------------------------------------------------------
 // Level 0: copyMakeBorder(image, 16, BORDER_REFLECT_101); one thread per 16-byte chunk of a
 // padded row (pitch is a multiple of 16).  Interior chunks (source columns [x-16, x) inside the
@@ -1901,9 +1901,10 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
             const int i = lane + 64 * j, r = i >> 2, c = i & 3;
             v[j] = src[i < NU ? __umul24((uint32_t)r, pu) + c : 0u];
         }
+        // all 192 units stored (units >= 172 repeat unit 0 into the buffer's unused tail,
+        // before the row-pass sums are written): no masked store
 #pragma unroll
-        for (int j = 0; j < 3; ++j)
-            if (lane + 64 * j < NU) ((uint4*)W)[lane + 64 * j] = v[j];
+        for (int j = 0; j < 3; ++j) ((uint4*)W)[lane + 64 * j] = v[j];
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS is in order per wave; compiler fence
     // IC_Angle (ORBextractor.cc:124-151): the disc sums m10 = sum u*I, m01 = sum v*I over
@@ -1916,18 +1917,18 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
         const int pc = x + 1 - xa;  // window column of patch column u = -15
         const int pd0 = pc >> 2, sh = pc & 3;
         const uint32_t* W32 = (const uint32_t*)W;
-        const uint32_t* mt = c_icmask + 288 * sh;
+        const uint32_t* mt = c_icmask + 320 * sh;
+        // five full 64-lane steps: dwords n >= 279 (patch rows 31 .. 35, still inside the
+        // 43-row window) carry zero masks, so no lane is masked off
 #pragma unroll
-        for (int j = 0; j < (31 * 9 + 63) / 64; ++j) {
+        for (int j = 0; j < 5; ++j) {
             const int n = lane + 64 * j;
-            if (n < 31 * 9) {
-                const int r = n / 9, c = n - r * 9;
-                const uint32_t pm = W32[(r + OD_WR - HALF_PATCH) * (OD_WP / 4) + pd0 + c] & mt[n];
-                const int S = (int)__builtin_amdgcn_udot4(pm, 0x01010101u, 0u, false);
-                const int T = (int)__builtin_amdgcn_udot4(pm, 0x03020100u, 0u, false);
-                m10 += __mul24(4 * c - sh - HALF_PATCH, S) + T;  // 24-bit multiplies: full-rate VALU
-                m01 += __mul24(r - HALF_PATCH, S);
-            }
+            const int r = n / 9, c = n - r * 9;
+            const uint32_t pm = W32[(r + OD_WR - HALF_PATCH) * (OD_WP / 4) + pd0 + c] & mt[n];
+            const int S = (int)__builtin_amdgcn_udot4(pm, 0x01010101u, 0u, false);
+            const int T = (int)__builtin_amdgcn_udot4(pm, 0x03020100u, 0u, false);
+            m10 += __mul24(4 * c - sh - HALF_PATCH, S) + T;  // 24-bit multiplies: full-rate VALU
+            m01 += __mul24(r - HALF_PATCH, S);
         }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // IC's window reads before the overlay writes
@@ -1941,7 +1942,13 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
         const int o0 = x - 5 - xa;  // 0..15, wave-uniform
         const int sb = o0 & 3, sd = o0 >> 2;
         const uint32_t* W32 = (const uint32_t*)W;
-        for (int task = lane; task < (OD_HPR / 2) * (OD_HC / 4); task += 64) {
+        static_assert((OD_HPR / 2) * (OD_HC / 4) == 110, "row-pass task count");
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+            // tasks 110 .. 127 of the second round repeat tasks 90 .. 107 of the same round
+            // (identical values to identical addresses): no lane is masked off
+            int task = lane + 64 * it;
+            if (task >= 110) task -= 20;
             const int rt = task / (OD_HC / 4), gq = task - rt * (OD_HC / 4);
             const int rq = OD_HPR / 2 - 1 - rt;
             uint32_t h[4][4];
@@ -3394,14 +3401,14 @@ static int upload_pattern(int device) {
             um[v] = v0;
             ++v0;
         }
-        uint32_t mt[4 * 288] = {};
+        uint32_t mt[4 * 320] = {};
         for (int sh = 0; sh < 4; ++sh)
             for (int n = 0; n < 31 * 9; ++n) {
                 const int r = n / 9, c = n % 9, v = std::abs(r - 15);
                 uint32_t m = 0;
                 for (int i = 0; i < 4; ++i)
                     if (std::abs(4 * c + i - sh - 15) <= um[v]) m |= 0xFFu << (8 * i);
-                mt[288 * sh + n] = m;
+                mt[320 * sh + n] = m;
             }
         HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_icmask), mt, sizeof(mt)));
     }
