@@ -882,7 +882,7 @@ __device__ __forceinline__ int fast_strength_packed(const uint8_t* p, int TP) {
 #define RR_Q 128  // per-wave queue of compass survivors (< 64 carried + 64 new), + a trash slot
 inline size_t rerun_lds(int dw, int dh) {
     const size_t dwp = (size_t)((dw + 3) & ~3), inW = (size_t)((3 + dw + 6 + 3) & ~3);
-    return 2 * dwp * dh + 4 * (size_t)((dh + 3) & ~3) + inW * (dh + 6) + 16 + 2 * (8 + 4 * (RR_Q + 8));
+    return 2 * dwp * dh + 4 * (size_t)((dh + 3) & ~3) + inW * (dh + 6) + 16 + 4 * (4 + 4 * (RR_Q + 8));
 }
 __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int dw, int dh, int rx0, int ry0, int t,
                                uint8_t* smem, uint32_t* __restrict__ out, int tid) {
@@ -909,7 +909,7 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
     // 12}: a necessary condition), survivors queued, the exact strength computed in full
     // 64-lane passes from the top of the queue (LDS accesses of one wave complete in order)
     {
-        uint16_t* q = (uint16_t*)(In + inW * (dh + 6)) + 8 + wave * (RR_Q + 8);  // after the staged ROI
+        uint32_t* q = (uint32_t*)(In + inW * (dh + 6)) + 4 + wave * (RR_Q + 8);  // after the staged ROI
         const uint32_t m = (uint32_t)((0x100000000ull + dw - 1) / (uint64_t)dw);  // i / dw = umulhi(i, m)
         const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
         const int total = dh * dw;
@@ -935,7 +935,7 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
                     Sp[yy * dwp + xx] = 0;
                 }
                 const uint64_t bm = __ballot(c);
-                q[c ? np + __popcll(bm & below) : RR_Q] = (uint16_t)i;  // RR_Q: trash slot
+                q[c ? np + __popcll(bm & below) : RR_Q] = (uint32_t)i;  // RR_Q: trash slot
                 np += __popcll(bm);
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1796,6 +1796,9 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
 //     border byte where the sample lies outside the ROI (in-place ROI blur: the padding stays
 //     un-blurred).  Exact integers throughout (T <= 257 * 65535 < 2^24).
 // No workgroup barrier: a wave reads only what it wrote (LDS is in order per wave).
+#ifndef OD_XCD  // 0: plain block order (experiments)
+#define OD_XCD 1
+#endif
 #define OD_WR 21   // window reach: rBRIEF |offset| <= 18 + the blur's 3
 #define OD_WP 64   // LDS row pitch of the raw window (bytes)
 #define OD_HC 40   // row-pass columns: x-18 .. x+21 (10 groups of 4)
@@ -1863,7 +1866,7 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
     // of keypoints (neighbouring keypoints share window rows: L2 hits instead of HBM re-reads)
     int bid = blockIdx.y * gridDim.x + blockIdx.x;
     const int full = (gridDim.x * gridDim.y) & ~7;
-    if (bid < full) bid = (bid & 7) * (full >> 3) + (bid >> 3);
+    if (OD_XCD && bid < full) bid = (bid & 7) * (full >> 3) + (bid >> 3);
     const int b = bid / gridDim.x;
     const int k = (bid - b * gridDim.x) * 4 + wave;  // slot: level l owns [kpBase_l, kpBase_l + nDesired_l)
     int l = 0;
