@@ -570,7 +570,9 @@ struct StreamGeom {
     int cap0;           // level-0 ring rows (row r in slot r % cap0)
 };
 #define PS_THREADS 1024
+#ifndef PS_LOADERS
 #define PS_LOADERS 2  // loader waves per workgroup
+#endif
 #define PS_NPF 8     // level-0 units (and row entries) per loader lane and round: K0 * u0 <= 1024
 #ifndef KR_STREAM_BATCH  // smallest batch that uses k_pyr_stream (one workgroup per frame)
 #define KR_STREAM_BATCH 256
