@@ -115,7 +115,7 @@ def pmc_traffic(kernel, workload, W, H, B, NF):
     if (w.get("width"), w.get("height"), w.get("batch"), w.get("nfeatures")) != (W, H, B, NF):
         return None, None, None
     k = d.get("per_launch", {}).get(kernel)
-    return (k["hbm_bytes"], d.get("source"), k.get("SQ_INSTS_VALU")) if k else (None, None, None)
+    return (k["hbm_bytes"], d.get("source"), k) if k else (None, None, None)
 
 
 def cpu_model():
@@ -494,7 +494,9 @@ def run_rank(args):
     frames_job = per * wl["streams"] if wl["streams"] else B * world  # every rank's frames of one step
 
     value = frames_job * args.steps / tmax
-    traffic, traffic_src, valu_insts = pmc_traffic(dom, args.workload, W, H, B, NF)
+    traffic, traffic_src, pmc = pmc_traffic(dom, args.workload, W, H, B, NF)
+    pmc = pmc or {}
+    valu_insts = pmc.get("SQ_INSTS_VALU")
     # VALU issue ceiling: each SIMD issues one wave64 VALU instruction per 2 cycles
     # (MI355X_MICROARCH.md), 4 SIMDs x 256 CUs at 2.4 GHz
     valu_peak = 256 * 4 / 2 * 2.4e9
@@ -540,6 +542,11 @@ def run_rank(args):
             "algorithmic_bytes_basis": "SURVEY.md §8d, this stage's terms only (bench.stage_bytes)",
             "valu_insts_per_launch": valu_insts,
             "valu_issue_frac": (valu_insts / (ds["ms_per_launch"] * 1e-3) / valu_peak) if valu_insts else None,
+            # the other issue ports of the same PMC pass: SALU (one per CU per cycle) and the LDS
+            # instructions with their bank-conflict cycles
+            "salu_insts_per_launch": pmc.get("SQ_INSTS_SALU"),
+            "lds_insts_per_launch": pmc.get("SQ_INSTS_LDS"),
+            "lds_bank_conflict_cycles_per_launch": pmc.get("SQ_LDS_BANK_CONFLICT"),
         },
         "pipeline": {
             "algorithmic_bytes_per_step": b_ext + b_match,
