@@ -125,3 +125,28 @@ def test_stream_pyramid_default_large_batch_sampled():
         for l in range(8):
             assert np.array_equal(got[l], ref[l]), f"frame {b} level {l}"
 
+
+
+@pytest.mark.parametrize("W,H,nf,sf,nl", [(1920, 1080, 3000, 1.2, 8), (1024, 768, 1500, 1.5, 5),
+                                          (800, 600, 1200, 1.25, 7)])
+def test_stream_pyramid_other_geometries(W, H, nf, sf, nl):
+    """Wider frames (smaller rounds) and other scale factors (other tap tables): the stream
+    plan, when the geometry has one, gives the per-level pyramid byte for byte."""
+    import torch
+
+    B = 2
+    frames = orb.synth_stream(W, H, stream=5, first=0, count=B)
+    ext = orb.ORBextractor(nf, sf, nl, orb.FAST_SCORE, 20, device=0, max_batch=B)
+    d = torch.from_numpy(frames).cuda()
+    ref = _run(ext, d, 1)
+    ok, k0, nr, lds = _plan(ext)
+    if not ok:
+        pytest.skip(f"no stream plan for {W}x{H} (per-level path only)")
+    got = _run(ext, d, 2)
+    for b in range(B):
+        for l in range(nl):
+            assert np.array_equal(got[3][b][l], ref[3][b][l]), f"frame {b} level {l}"
+        n = ref[2][b]
+        assert got[2][b] == n and got[0][b, :n].tobytes() == ref[0][b, :n].tobytes()
+        assert got[1][b, :n].tobytes() == ref[1][b, :n].tobytes()
+    orb.hip_lib().orb_debug_set_pyramid_path(ext._h, 0)
