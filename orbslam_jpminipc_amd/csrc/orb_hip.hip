@@ -689,7 +689,7 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
         // {source row 0, source row 1 (LDS addresses), b0 << 12, b1 << 12, own ring row (LDS
         //  address, ~0u: none), padded-row offset, top mirror offset, bottom mirror offset (~0u: none)}
         const uint4* E = rowEntries + 2 * ((int)rounds[n * rw + sg.L] + (int)(e >> 18));
-        if (cnt > 0 && myL == 0) {
+        if (cnt > 0 && myL == 0 && PS_EXP != 5) {
             // padded level-0 rows from the ring (k_pyr0's copyMakeBorder), 16 B per unit
             for (int c = ql; c < nq; c += qs) {
                 const int px = 16 * c;
@@ -698,8 +698,21 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
                     const uint4 e0 = E[2 * k], e1 = E[2 * k + 1];
                     const uint8_t* R = s_ring + e0.x;
                     uint4 v;
-                    if (inner) {
-                        v = *(const uint4*)(R + px - EDGE);
+                    if (inner || PS_EXP == 4) {
+                        v = *(const uint4*)(R + (PS_EXP == 4 ? max(px - EDGE, 0) : px - EDGE));
+                    } else if (px == 0) {
+                        // left border: bytes R[16], R[15], .. R[1] (reflect-101 of -16 .. -1),
+                        // the aligned dwords R[0..19] reversed by v_perm
+                        const uint4 a = *(const uint4*)R;
+                        const uint32_t a4 = *(const uint32_t*)(R + 16);
+                        v = make_uint4(__builtin_amdgcn_perm(a4, a.w, 0x01020304u), __builtin_amdgcn_perm(a.w, a.z, 0x01020304u),
+                                       __builtin_amdgcn_perm(a.z, a.y, 0x01020304u), __builtin_amdgcn_perm(a.y, a.x, 0x01020304u));
+                    } else if ((w & 15) == 0 && px == w + EDGE) {
+                        // right border of a 16-aligned row: R[w-2], R[w-3], .. R[w-17], from the
+                        // aligned dwords R[w-32 .. w-1] (E0 .. E7) reversed by v_perm
+                        const uint4 lo = *(const uint4*)(R + w - 32), hi = *(const uint4*)(R + w - 16);
+                        v = make_uint4(__builtin_amdgcn_perm(hi.w, hi.z, 0x03040506u), __builtin_amdgcn_perm(hi.z, hi.y, 0x03040506u),
+                                       __builtin_amdgcn_perm(hi.y, hi.x, 0x03040506u), __builtin_amdgcn_perm(hi.x, lo.w, 0x03040506u));
                     } else {  // a border unit: single-bounce reflect-101 (w >= 17); all 16
                               // reads unconditional (clamped), so they issue back to back
                         uint32_t by[16];
