@@ -854,16 +854,24 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
 // ---- FAST strength --------------------------------------------------------------------------
 // S(p) = 1 + cornerScore<16>(p) of cv::FAST: the largest t for which p is a corner is S - 1,
 // so p is a corner at threshold t <=> S > t; records carry S - 1 as the score.
-// Both sides in one packed register: lane 0 of each i16x2 carries the
-// dark contrast v - c, lane 1 the bright contrast c - v; arcs of 9 by doubling windows
-// (2, then 2+2+2+2+1), both sides per instruction.  ~130 VALU and 16 registers of
-// circle values: cheap enough to run on every pre-filter survivor instead of a 9-arc test
-// followed by a second gather for the corners (k_fast's queue is LDS-latency bound).
+// Both sides in one packed register of two exact f16 integers: lane 0 carries the dark
+// contrast v - c, lane 1 the bright contrast c - v.  A byte b is the f16 1024 + b (bits
+// 0x6400 | b), so (1024 + v, 1024 + c) is one v_lshl_or and the pair of contrasts one
+// v_pk_add_f16 with swapped, negated operand halves; all values are integers in [-255, 255],
+// exact in f16.  Arcs of 9 as windows of 3 (two v_pk_minimum3_f16 per arc, gfx950), the
+// best arc by v_pk_maximum3_f16: ~75 VALU per pixel, half the i16 version's.  Cheap enough to
+// run on every pre-filter survivor instead of a 9-arc test followed by a second gather for the
+// corners (k_fast's queue is LDS-latency bound).
+#ifndef FS_I16  // 1: the previous i16 arithmetic (experiments)
+#define FS_I16 0
+#endif
 typedef short s16x2_t __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ int fast_strength_packed(const uint8_t* p, int TP) {
     const int off[16] = {3 * TP, 3 * TP + 1, 2 * TP + 2, TP + 3, 3, -TP + 3, -2 * TP + 2, -3 * TP + 1,
                          -3 * TP, -3 * TP - 1, -2 * TP - 2, -TP - 3, -3, TP - 3, 2 * TP - 2, 3 * TP - 1};
     const uint32_t v = p[0];
+#if FS_I16
     s16x2_t d[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
@@ -871,7 +879,6 @@ __device__ __forceinline__ int fast_strength_packed(const uint8_t* p, int TP) {
         // (v, c) - (c, v) = (v - c, c - v)
         d[k] = __builtin_bit_cast(s16x2_t, v | (c << 16)) - __builtin_bit_cast(s16x2_t, c | (v << 16));
     }
-    // windows of 2, then 9 = 2+2+2+2+1 (two register arrays live, not three)
     s16x2_t m2[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) m2[k] = __builtin_elementwise_min(d[k], d[(k + 1) & 15]);
@@ -885,6 +892,27 @@ __device__ __forceinline__ int fast_strength_packed(const uint8_t* p, int TP) {
         best = k ? __builtin_elementwise_max(best, w9) : w9;
     }
     return max((int)best.x, (int)best.y);
+#else
+    const uint32_t V = 0x64006400u | v;
+    f16x2_t d[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const f16x2_t P = __builtin_bit_cast(f16x2_t, V | ((uint32_t)p[off[k]] << 16));  // (1024+v, 1024+c)
+        d[k] = P - __builtin_shufflevector(P, P, 1, 0);                                  // (v - c, c - v)
+    }
+    f16x2_t m3[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        m3[k] = __builtin_elementwise_minimum(__builtin_elementwise_minimum(d[k], d[(k + 1) & 15]), d[(k + 2) & 15]);
+    f16x2_t best = __builtin_elementwise_minimum(__builtin_elementwise_minimum(m3[0], m3[3]), m3[6]);
+#pragma unroll
+    for (int k = 1; k < 16; k += 2) {
+        const f16x2_t a = __builtin_elementwise_minimum(__builtin_elementwise_minimum(m3[k], m3[(k + 3) & 15]), m3[(k + 6) & 15]);
+        const f16x2_t c = k + 1 < 16 ? __builtin_elementwise_minimum(__builtin_elementwise_minimum(m3[k + 1], m3[(k + 4) & 15]), m3[(k + 7) & 15]) : a;
+        best = __builtin_elementwise_maximum(__builtin_elementwise_maximum(best, a), c);
+    }
+    return max((int)best.x, (int)best.y);
+#endif
 }
 
 // The reference's `FAST(cellImage, keys, 7, true)` re-run of a cell that kept <= 3 corners at
