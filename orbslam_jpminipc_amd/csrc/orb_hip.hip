@@ -1843,10 +1843,16 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
 #define OD_XCD 1
 #endif
 #define OD_WR 21   // window reach: rBRIEF |offset| <= 18 + the blur's 3
-#define OD_WP 64   // LDS row pitch of the raw window (bytes)
+#ifndef OD_WP
+#define OD_WP 64   // LDS row pitch of the raw window (bytes).  80 (row blocks 4 rows apart on
+                   // different banks: the row pass's 7-way conflicts become 2-way) measured
+                   // slower: 640x480 0.607 vs 0.597 ms, 1241x376 1.183 vs 1.172
+#endif
 #define OD_HC 40   // row-pass columns: x-18 .. x+21 (10 groups of 4)
 #define OD_HPR 22  // row pairs of the row-pass sums (window rows 0 .. 43)
-#define OD_HOFF 128  // byte offset of the sums in the wave's buffer (see the row pass)
+// byte offset of the sums in the wave's buffer: the first row-pass round's writes (from byte
+// OD_HOFF + 160 * 8) must stay above window row 20, the last one the second round reads
+#define OD_HOFF (OD_WP == 64 ? 128 : 21 * OD_WP - 8 * 160)
 #define GT_WA 0x37312212u  // bytes (x-3, x-2, x-1, x) -> 18, 34, 49, 55
 #define GT_WB 0x00122231u  // bytes (x+1, x+2, x+3, x+4) -> 49, 34, 18, 0
 // column-pass taps over row pairs (low half = the even row): rows r0-3 .. r0+4 when r0 is even
@@ -1949,8 +1955,13 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
         }
         // all 192 units stored (units >= 172 repeat unit 0 into the buffer's unused tail,
         // before the row-pass sums are written): no masked store
+        static_assert(48 * OD_WP <= OD_HOFF + OD_HPR * OD_HC * 4, "window tail inside the wave's buffer");
+        static_assert(OD_HOFF + 8 * 160 >= 20 * OD_WP, "first-round sums above the second round's rows");
 #pragma unroll
-        for (int j = 0; j < 3; ++j) ((uint4*)W)[lane + 64 * j] = v[j];
+        for (int j = 0; j < 3; ++j) {
+            const int i = lane + 64 * j;
+            ((uint4*)W)[(i >> 2) * (OD_WP / 16) + (i & 3)] = v[j];
+        }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS is in order per wave; compiler fence
     // IC_Angle (ORBextractor.cc:124-151): the disc sums m10 = sum u*I, m01 = sum v*I over
