@@ -1,0 +1,95 @@
+"""The FAST strength arithmetic of `fast_strength_packed` (orb_hip.hip): contrasts as exact f16
+integers (a byte b is the f16 1024 + b), arcs of 9 as three windows of 3 (the kernel's
+v_pk_minimum3_f16), the best arc by maximum.  Emulated here in numpy float16 (IEEE binary16,
+the same rounding as the hardware) and checked (1) to stay exact: every intermediate equals
+the integer value; (2) to give S = 1 + cornerScore of cv::FAST, against the oracle's FAST
+(ORBextractor.cc:602 `FAST(..., true)`) on 7x7 patches: a corner at threshold t
+iff S > t, response S - 1."""
+import ctypes
+
+import numpy as np
+
+from oracle_lib import lib
+
+# circle order of the kernel's off[16] table: (dy, dx)
+CIRCLE = [(3, 0), (3, 1), (2, 2), (1, 3), (0, 3), (-1, 3), (-2, 2), (-3, 1),
+          (-3, 0), (-3, -1), (-2, -2), (-1, -3), (0, -3), (1, -3), (2, -2), (3, -1)]
+
+
+def _arcs(d):
+    """max over the 16 arcs of 9 of the arc minimum, by windows of 3 (d: (N, 16))."""
+    m3 = np.minimum(np.minimum(d, np.roll(d, -1, axis=1)), np.roll(d, -2, axis=1))
+    w9 = np.minimum(np.minimum(m3, np.roll(m3, -3, axis=1)), np.roll(m3, -6, axis=1))
+    return w9.max(axis=1), m3, w9
+
+
+def strength_f16(v, c):
+    V = (1024 + v.astype(np.int32)).astype(np.float16)[:, None]
+    C = (1024 + c.astype(np.int32)).astype(np.float16)
+    out, inter = [], []
+    for d in (V - C, C - V):  # (v - c, c - v): the kernel's two f16 lanes
+        best, m3, w9 = _arcs(d)
+        out.append(best)
+        inter += [d, m3, w9, best]
+    return np.maximum(out[0], out[1]), inter
+
+
+def strength_int(v, c):
+    vi = v.astype(np.int32)[:, None]
+    ci = c.astype(np.int32)
+    out, inter = [], []
+    for d in (vi - ci, ci - vi):
+        best, m3, w9 = _arcs(d)
+        out.append(best)
+        inter += [d, m3, w9, best]
+    return np.maximum(out[0], out[1]), inter
+
+
+def _cases(n, seed):
+    rng = np.random.default_rng(seed)
+    v = rng.integers(0, 256, n).astype(np.uint8)
+    c = rng.integers(0, 256, (n, 16)).astype(np.uint8)
+    # corner-like rings: a bright or dark arc of 9..16 around v, the rest random
+    k = rng.integers(0, 16, n)
+    ln = rng.integers(9, 17, n)
+    sign = rng.choice([-1, 1], n)
+    for i in range(n // 2):
+        for j in range(ln[i]):
+            c[i, (k[i] + j) % 16] = np.clip(int(v[i]) + sign[i] * rng.integers(1, 200), 0, 255)
+    # extremes
+    v[:256] = np.arange(256)
+    c[:128] = 0
+    c[128:256] = 255
+    return v, c
+
+
+def test_f16_strength_is_exact():
+    v, c = _cases(20000, 1)
+    sf, inf = strength_f16(v, c)
+    si, ini = strength_int(v, c)
+    for a, b in zip(inf, ini):
+        assert np.array_equal(a.astype(np.int32), b), "an f16 intermediate is not the exact integer"
+    assert np.array_equal(sf.astype(np.int32), si)
+    assert si.min() >= -255 and si.max() <= 255
+
+
+def test_f16_strength_is_cornerscore_plus_one():
+    v, c = _cases(3000, 2)
+    S = strength_f16(v, c)[0].astype(np.int32)
+    rng = np.random.default_rng(3)
+    L = lib()
+    out = np.zeros(3 * 4, np.int32)
+    n_corner = 0
+    for i in range(len(v)):
+        p = np.zeros((7, 7), np.uint8)
+        p[3, 3] = v[i]
+        for k, (dy, dx) in enumerate(CIRCLE):
+            p[3 + dy, 3 + dx] = c[i, k]
+        t = int(rng.integers(1, 80))
+        n = L.oracle_fast(p.ctypes.data_as(ctypes.c_void_p), 7, 7, 7, t,
+                          out.ctypes.data_as(ctypes.c_void_p), 4)
+        assert n == (1 if S[i] > t else 0), f"case {i}: S {S[i]}, t {t}, oracle corners {n}"
+        if n:
+            n_corner += 1
+            assert (out[0], out[1]) == (3, 3) and out[2] == S[i] - 1, f"case {i}: response {out[2]} vs S-1 {S[i] - 1}"
+    assert n_corner > 300  # the corner-like half is exercised
