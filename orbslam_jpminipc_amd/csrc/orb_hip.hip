@@ -1076,6 +1076,9 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
 // deciding later still counts the cell among the fallback cells (the ordinal -> workgroup
 // assignment is the same everywhere, and so is the decision of every wave of a workgroup).
 // Large batches keep the re-runs inside k_select<.., true>: there every CU is busy anyway.
+#ifndef KR_NWG_MIN  // least k_rerun workgroups per (frame, level): at B = 512, 1 / 2 / 3 / 4 measured
+#define KR_NWG_MIN 3  // re-runs + selection 640x480 0.146 / 0.117 / 0.116 / 0.132 ms, 1241x376
+#endif                // 0.463 / 0.380 / 0.357 / 0.406, 1280x720 0.814 / 0.809 / 0.765 / 0.910
 #define RERUN_FLAG 0x40000000
 #define COUNT_MASK 0x3FFFFFFF
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_rerun(const uint8_t* __restrict__ pyr, uint32_t* __restrict__ cand,
@@ -3409,7 +3412,7 @@ struct orb_extractor {
         // 640x480 0.190 vs 0.239 ms inside; 1241x376 0.497 vs 0.696; 1280x720 0.864 vs 1.421).
         const bool sep = (B < KS_SEP_BATCH || (long long)W * H > KS_SEP_PIXELS) && cellLds;
         if (sep && !KS_SKIP_RERUN) {
-            const int NWG = std::min(32, std::max(1, 512 / (B * nlevels)));
+            const int NWG = std::min(32, std::max(KR_NWG_MIN, 512 / (B * nlevels)));
             hipLaunchKernelGGL(k_rerun, dim3(B * NWG, nlevels), dim3(256), cellLds, st, d_pyr, d_cand, d_cellCount, g,
                                d_cells, NWG);
         }
