@@ -1081,7 +1081,12 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
 #endif                // 0.463 / 0.380 / 0.357 / 0.406, 1280x720 0.814 / 0.809 / 0.765 / 0.910
 #define RERUN_FLAG 0x40000000
 #define COUNT_MASK 0x3FFFFFFF
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_rerun(const uint8_t* __restrict__ pyr, uint32_t* __restrict__ cand,
+#ifndef KR_WAVES
+#define KR_WAVES 4  // waves per SIMD k_rerun's register allocation targets; re-runs + selection at
+                    // B = 512 with 2 / 3 / 5 / 6 / 8: 1241x376 0.406 / 0.404 / 0.434 / 0.437 /
+                    // 0.453 ms vs 0.357, 1280x720 0.90-1.17 vs 0.765
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KR_WAVES))) k_rerun(const uint8_t* __restrict__ pyr, uint32_t* __restrict__ cand,
                                                int* __restrict__ cellCount, Geom g,
                                                const CellGeom* __restrict__ cells, int NWG) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
