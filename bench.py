@@ -128,9 +128,44 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(frames, nfeatures, threads, W, H):
+def host_cpus():
+    """What this process may run on: the affinity set (the threads the CPU baseline uses by
+    default), the machine's logical CPU count, the cgroup v2 CPU quota (cpu.max, in CPUs; None
+    when unlimited or absent) and OMP_NUM_THREADS as set by the environment."""
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    return {"affinity": affinity, "logical_cpus": os.cpu_count(), "cgroup_cpu_quota": quota,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
+def physical_cores():
+    """Physical cores of the machine from /proc/cpuinfo (distinct (physical id, core id))."""
+    cores, phys = set(), "0"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("physical id"):
+                phys = line.split(":", 1)[1].strip()
+            elif line.startswith("core id"):
+                cores.add((phys, line.split(":", 1)[1].strip()))
+    except OSError:
+        pass
+    return len(cores) or None
+
+
+def cpu_baseline(frames, nfeatures, threads, W, H, quota_threads=None):
     """Oracle (test infrastructure, oracle/liborb_oracle.so) on a bounded sample: extract-only
-    and extract+match frames/s on `threads` threads, single-thread ms/frame."""
+    and extract+match frames/s on `threads` threads (and on `quota_threads` threads, when the
+    cgroup caps CPU time below the affinity set), single-thread ms/frame."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import ctypes
 
@@ -155,7 +190,12 @@ def cpu_baseline(frames, nfeatures, threads, W, H):
     n1 = min(len(fr), 48)
     t_one = run(fr[:n1], 1, 0)
     t_one_m = run(fr[:n1], 1, 1)
+    extra = {}
+    if quota_threads and quota_threads < threads:
+        tq = run(fr, quota_threads, 1)
+        extra = {"quota_threads": quota_threads, "quota_threads_extract_match_fps": len(fr) / tq}
     return {
+        **extra,
         "extract_fps": len(fr) / t_ext,
         "extract_match_fps": len(fr) / t_all,
         "single_thread_ms_per_frame_extract": t_one / n1 * 1e3,
@@ -187,11 +227,32 @@ def launch_replicas(n):
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
                                       stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
-    out0 = procs[0].communicate()[0]
-    rcs = [procs[0].returncode] + [p.wait() for p in procs[1:]]
-    sys.stdout.write(out0.decode())
+    # rank 0's output is drained on a thread while every rank is polled: a rank that dies early
+    # would otherwise leave the others blocked in the rendezvous or the barrier
+    import threading
+
+    chunks = []
+    reader = threading.Thread(target=lambda: chunks.append(procs[0].stdout.read()), daemon=True)
+    reader.start()
+    failed = 0
+    while any(p.poll() is None for p in procs):
+        bad = next((p.returncode for p in procs if p.returncode not in (None, 0)), 0)
+        if bad:
+            failed = bad
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+            break
+        time.sleep(0.05)
+    reader.join(timeout=30)
+    sys.stdout.write(b"".join(chunks).decode())
     sys.stdout.flush()
-    return next((rc for rc in rcs if rc), 0)
+    return failed or next((p.returncode for p in procs if p.returncode), 0)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -296,8 +357,9 @@ def latency_b1(orb, W, H, NF, device, frames, reps=100):
         "cpu_oracle_single_thread_sfi_ms": c_sfi * 1e3,
         "note": f"{W}x{H}, {NF} kp, {reps} calls each through the Python binding (ctypes); host entries include "
                 "the H2D/D2H copies through the handle's pinned staging and one stream synchronisation per call; "
-                "batches below 32 / 256 frames run the FAST(7) re-runs / the small pyramid levels with "
-                "per-level multi-workgroup launches (k_rerun, k_pyr_resize)",
+                "the FAST(7) re-runs always run in k_rerun (more workgroups per (frame, level) at small "
+                "batches), and batches below 256 frames build the pyramid with per-level launches "
+                "(k_pyr0, k_pyr_resize)",
     }
 
 
@@ -500,6 +562,15 @@ def run_rank(args):
     # VALU issue ceiling: each SIMD issues one wave64 VALU instruction per 2 cycles
     # (MI355X_MICROARCH.md), 4 SIMDs x 256 CUs at 2.4 GHz
     valu_peak = 256 * 4 / 2 * 2.4e9
+    # the roof that actually binds the dominant kernel: the larger of its VALU-issue fraction
+    # and its PMC-measured HBM fraction (the algorithmic-bytes fraction below is the contract's
+    # HBM roofline figure; it is not what limits these integer kernels)
+    roofs = {}
+    if valu_insts:
+        roofs["valu_issue"] = valu_insts / (ds["ms_per_launch"] * 1e-3) / valu_peak
+    if traffic:
+        roofs["hbm_measured_traffic"] = traffic / (ds["ms_per_launch"] * 1e-3) / 1e9 / HBM_PEAK_GBS
+    binding = max(roofs, key=roofs.get) if roofs else None
     label = wl["label"] if not custom else f"custom {W}x{H}, ORBextractor({NF},1.2,8,FAST,20) + SearchForInitialization"
     result = {
         "metric": METRIC,
@@ -547,6 +618,12 @@ def run_rank(args):
             "salu_insts_per_launch": pmc.get("SQ_INSTS_SALU"),
             "lds_insts_per_launch": pmc.get("SQ_INSTS_LDS"),
             "lds_bank_conflict_cycles_per_launch": pmc.get("SQ_LDS_BANK_CONFLICT"),
+            "binding": binding,
+            "binding_frac": roofs.get(binding) if binding else None,
+            "roofs": roofs,
+            "bound_note": "bound/frac price the kernel against the HBM roofline with SURVEY §8d algorithmic "
+                          "bytes (the contract's figure); `binding` names the roof that limits it, from the "
+                          "same PMC pass",
         },
         "pipeline": {
             "algorithmic_bytes_per_step": b_ext + b_match,
@@ -563,10 +640,14 @@ def run_rank(args):
     if rank == 0 and world == 1 and args.latency:
         result["latency_b1"] = latency_b1(orb, W, H, NF, local, frames[:2])
     if rank == 0 and world == 1 and args.cpu_frames > 0:
-        threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or os.cpu_count())
-        ncpu = args.cpu_frames
+        hc = host_cpus()
+        # every core the process may use (north_star: "all host cores, count stated")
+        threads = args.cpu_threads or hc["affinity"]
+        ncpu = max(args.cpu_frames, 4 * threads)  # at least 4 frames per thread
         cpu_frames = orb.synth_stream(W, H, stream=0, first=0, count=ncpu)
-        cb = cpu_baseline(cpu_frames, NF, threads, W, H)
+        quota = hc["cgroup_cpu_quota"]
+        cb = cpu_baseline(cpu_frames, NF, threads, W, H, int(quota) if quota and quota >= 1 else None)
+        pcores = physical_cores()
         result["cpu_baseline"] = {
             "value": cb["extract_match_fps"],
             "unit": "frames/s",
@@ -580,9 +661,25 @@ def run_rank(args):
             "single_thread_ms_per_frame_extract_match": cb["single_thread_ms_per_frame_extract_match"],
             "single_thread_sample_frames": cb["single_thread_sample_frames"],
             "cpu_model": cpu_model(),
-            "logical_cpus_visible": os.cpu_count(),
+            "logical_cpus_visible": hc["logical_cpus"],
+            "affinity_cpus": hc["affinity"],
+            "cgroup_cpu_quota": hc["cgroup_cpu_quota"],
+            "omp_num_threads_env": hc["omp_num_threads"],
+            "cores_note": "threads = the process's CPU affinity set (every core it may run on)"
+                          + ("" if hc["cgroup_cpu_quota"] is None else
+                             f"; the cgroup caps CPU time at {hc['cgroup_cpu_quota']:g} CPUs, so the "
+                             "threads share that quota"),
             "wall_s": cb["wall_s"],
         }
+        if "quota_threads" in cb:
+            result["cpu_baseline"]["at_quota_threads"] = {
+                "threads": cb["quota_threads"], "extract_match_fps": cb["quota_threads_extract_match_fps"]}
+        if pcores:
+            # what the whole socket would reach if every physical core ran the single-thread rate
+            # (no SMT gain, no memory contention): an estimate for the ratio, not a measurement
+            result["cpu_baseline"]["machine_physical_cores"] = pcores
+            result["cpu_baseline"]["estimate_all_physical_cores_fps"] = (
+                pcores * 1e3 / cb["single_thread_ms_per_frame_extract_match"])
     if rank == 0:
         print(json.dumps(result))
     replicas.shutdown(info)
@@ -602,12 +699,12 @@ def main():
     ap.add_argument("--height", type=int, default=0)
     ap.add_argument("--nfeatures", type=int, default=0)
     ap.add_argument("--cpu-frames", type=int, default=1536,
-                    help="CPU-baseline sample size (0 = skip); ~10 s of oracle wall time on 16 threads")
+                    help="CPU-baseline sample size (0 = skip; at least 4 frames per thread)")
     ap.add_argument("--latency", type=int, default=1, help="1: measure latency_b1 (rank 0, N = 1)")
     ap.add_argument("--overlap", type=int, default=0,
                     help="0 (default): serial step; 1 / 2: stream-overlap experiments, measured slower")
     ap.add_argument("--survey-steps", type=int, default=5, help="untimed steps with every stage bracketed")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = OMP_NUM_THREADS or os.cpu_count()")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU of the affinity set")
     ap.add_argument("--dry-run", action="store_true", help="CPU only: launcher + rank plumbing with the oracle")
     args = ap.parse_args()
     args.survey_steps = max(1, args.survey_steps)

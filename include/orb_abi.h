@@ -137,9 +137,12 @@ int orb_search_for_initialization(const orb_keypoint_t* kps1, const uint8_t* des
  *   d_prev_xy: P x cap x 2 floats (in/out); NULL means "vbPrevMatched = F1 keypoints"
  *              (Tracking::FirstInitialization, reference Tracking.cc:366-368) and no update.
  *   d_matches12: P x cap int32; d_nmatches: P int32.  Asynchronous on `stream`.
- * cap <= 8192.  Frames with up to 1024 octave-0 keypoints are matched with all state in LDS;
- * pairs over that (e.g. the reference init extractor, nFeatures*2, at 1280x720) are redone by a
- * large-capacity kernel on the same stream (stream-ordered scratch), so every pair is exact. */
+ * cap <= 8192.  One workgroup per pair holds up to nmax octave-0 keypoints per frame in LDS:
+ * nmax = min(cap, 1024) for P < 256 pairs, min(cap, 1024, max(256, ~9/40 cap)) otherwise (the
+ * extractor keeps at most 0.217 nFeatures at level 0).  A pair over nmax (another producer, the
+ * reference init extractor's nFeatures*2 at 1280x720) is redone exactly by the same workgroup
+ * with its staged arrays in a grow-only scratch kept per (device, stream); every pair is exact
+ * and there is one launch per call. */
 int orb_search_for_initialization_batch_device(const orb_keypoint_t* d_kps, const uint8_t* d_desc,
                                                const int32_t* d_counts, int cap, int P, const int32_t* d_pair_f1,
                                                const int32_t* d_pair_f2, orb_frame_bounds_t bounds, float nnratio,
@@ -442,9 +445,6 @@ int orb_debug_level_image(orb_extractor_t* h, int b, int l, uint8_t* out, int* w
  * cell grid lets keypoints sit past the FAST border) (device sync). */
 int orb_debug_blur_image(orb_extractor_t* h, int b, int l, uint8_t* out);
 /* Per-cell FAST keypoint counts of frame b, level l (device sync); returns #cells. */
-/* Retired FAST-queue statistics hook of round 1's k_level (kept for ABI stability): writes
- * three zeros. */
-int orb_debug_klevel_counts(unsigned long long* out3);
 int orb_debug_cell_counts(orb_extractor_t* h, int b, int l, int* counts, int cap);
 /* Pyramid kernels used by the next extractions (results are identical): 0 = automatic (the
  * one-pass streaming kernel k_pyr_stream for batches >= 256 grey frames, per-level launches

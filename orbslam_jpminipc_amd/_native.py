@@ -182,7 +182,6 @@ HIP_SIGNATURES = {
     "orb_debug_nth_element_wave_u32": (_i, [_vp, _i, _i, _i]),
     "orb_debug_level_image": (_i, [_vp, _i, _i, _vp, ctypes.POINTER(_i), ctypes.POINTER(_i)]),
     "orb_debug_cell_counts": (_i, [_vp, _i, _i, _vp, _i]),
-    "orb_debug_klevel_counts": (_i, [_vp]),
     "orb_debug_blur_image": (_i, [_vp, _i, _i, _vp]),
     "orb_debug_set_pyramid_path": (_i, [_vp, _i]),
     "orb_debug_pyramid_plan": (_i, [_vp, _pi, _pi, _pi]),

@@ -6,8 +6,8 @@
 //                 (k_pyr_resize_tail: the small levels of a large batch in one launch)
 //   k_fast        per level tile: FAST strength at fastTh and the per-cell 3x3 NMS; survivors
 //                 appended to their cell's slots          (ORBextractor.cc:560-607)
-//   k_rerun       FAST(7) re-run of cells with <= 3 survivors (609-614), spread over many
-//                 workgroups (few or large frames; otherwise inside k_select)
+//   k_rerun       FAST(7) re-run of cells with <= 3 survivors (609-614), spread over several
+//                 workgroups per (frame, level)
 //   k_select      per (frame, level): raster order per cell, quota redistribution, retainBest
 //                 per cell and per level — exact libstdc++ nth_element replay (622-701)
 //   k_orient_desc per keypoint (one wave): IC angle on the raw level, rBRIEF on the
@@ -36,14 +36,6 @@
 #define ORB_MAX_LEVELS 16
 #define ORB_MAX_CELLS_PER_LEVEL 256
 #define ORB_SELECT_LDS_CAP 6144
-// k_fast phase switches: timing experiments only (scripts/klevel_phases.sh builds variants
-// with -DKL_SKIP_*=1 into build/variants); the product build leaves them 0.
-#ifndef KL_SKIP_FAST
-#define KL_SKIP_FAST 0
-#endif
-#ifndef KL_SKIP_QUEUE
-#define KL_SKIP_QUEUE 0
-#endif
 #ifndef KF_TIMING  // 1: per-phase s_memtime sums of k_fast's waves (experiment builds only)
 #define KF_TIMING 0
 #endif
@@ -53,15 +45,11 @@ __device__ unsigned long long g_kftime[8];
 #else
 #define KF_T(i)
 #endif
-// k_select ablations (timing-only, likewise): FAST(7) re-run, per-cell and per-level retainBest
-#ifndef KS_SKIP_RERUN
-#define KS_SKIP_RERUN 0
-#endif
-#ifndef KS_SKIP_RETAIN
-#define KS_SKIP_RETAIN 0
-#endif
-#ifndef KS_SKIP_LEVEL_RETAIN
-#define KS_SKIP_LEVEL_RETAIN 0
+// Only switches that keep the output exact (sizes, register targets, timing probes) exist in
+// this translation unit; ablations that change the output are not part of the product source.
+#if defined(KL_SKIP_FAST) || defined(KL_SKIP_QUEUE) || defined(KS_SKIP_RERUN) || defined(KS_SKIP_RETAIN) || \
+    defined(KS_SKIP_LEVEL_RETAIN) || defined(KF_NOATOMIC) || defined(KM_SKIP1) || defined(KM_SKIP2)
+#error "wrong-output ablation switches were removed from the product source"
 #endif
 
 // ======================================================================================
@@ -1067,15 +1055,15 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
     return total;
 }
 
-// The FAST(7) re-runs of every (frame, level) for small batches (the per-frame latency path),
-// before k_select<.., false>: NWG workgroups per (frame, level), workgroup (b * NWG + gw, l)
+// The FAST(7) re-runs of every (frame, level), at every batch size, before k_select<.., false>
+// (the in-k_select re-run path, k_select<.., true>, is kept only for -DKS_SEP_PIXELS
+// experiments): NWG workgroups per (frame, level), workgroup (b * NWG + gw, l)
 // re-running the level's fallback cells gw, gw + NWG, ... (in cell order), so one frame's
 // re-runs — serial inside k_select's single workgroup per level — spread over many CUs.  A
 // cell re-runs where the reference's does: not skipped, and min(count, cap) <= 3 with 0 for a
 // cell with no detection area.  The new count is stored with RERUN_FLAG set, so a workgroup
 // deciding later still counts the cell among the fallback cells (the ordinal -> workgroup
 // assignment is the same everywhere, and so is the decision of every wave of a workgroup).
-// Large batches keep the re-runs inside k_select<.., true>: there every CU is busy anyway.
 #ifndef KR_NWG_MIN  // least k_rerun workgroups per (frame, level): at B = 512, 1 / 2 / 3 / 4 measured
 #define KR_NWG_MIN 3  // re-runs + selection 640x480 0.146 / 0.117 / 0.116 / 0.132 ms, 1241x376
 #endif                // 0.463 / 0.380 / 0.357 / 0.406, 1280x720 0.814 / 0.809 / 0.765 / 0.910
@@ -1293,7 +1281,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
     // (1) FAST(cellImage, keys, 7, true) where a cell kept <= 3 (a skipped cell is `continue`d)
     {
         const int nfb = s_fb[ORB_MAX_CELLS_PER_LEVEL];
-        for (int f = 0; f < (RERUN && !KS_SKIP_RERUN ? nfb : 0); ++f) {
+        for (int f = 0; f < (RERUN ? nfb : 0); ++f) {
             const int c = s_fb[f];
             const CellGeom cg = lc[c];
             const int dw = cg.hx - 6, dh = cg.hy - 6;
@@ -1475,7 +1463,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
     // serial replays run on four SIMDs instead of one wave's lanes
     for (int c = KS_CELL_SPREAD ? lane * 4 + wave : tid; c < nC; c += 256) {
         uint32_t* seg = srt + (inLds ? s_off[c] : lc[c].candOff);
-        s_cnt[c] = KS_SKIP_RETAIN ? min(s_cnt[c], max(s_ret[c], 0)) : orbsel::retain_best(seg, s_cnt[c], s_ret[c], comp);
+        s_cnt[c] = orbsel::retain_best(seg, s_cnt[c], s_ret[c], comp);
     }
     __syncthreads();
     if (wave == 0) wave_prefix(s_koff, s_cnt, nC, lane);
@@ -1502,9 +1490,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
         keep = lg.nDesired;
         if (inLds) {  // one wave, partitions by ballot (nth_select.h); scratch = the free srt region
             uint16_t* Lp = (uint16_t*)srt;
-            if (wave == 0 && !KS_SKIP_LEVEL_RETAIN)
+            if (wave == 0)
                 orbsel::retain_best_wave(list, K, lg.nDesired, comp, Lp, Lp + K, lane);
-        } else if (tid == 0 && !KS_SKIP_LEVEL_RETAIN) {
+        } else if (tid == 0) {
             orbsel::retain_best(list, K, lg.nDesired, comp);
         }
     }
@@ -1584,9 +1572,6 @@ __device__ __forceinline__ uint32_t compass4(uint32_t c, uint32_t q0, uint32_t q
     return ((pass[0] >> 15) & 1u) | ((pass[1] >> 14) & 2u) | ((pass[0] >> 29) & 4u) | ((pass[1] >> 28) & 8u);
 }
 
-#ifndef KF_NOATOMIC  // timing experiment only (wrong output): survivors stored without the slot atomic
-#define KF_NOATOMIC 0
-#endif
 #ifndef KF_WAVES
 #define KF_WAVES 0  // > 0: waves per SIMD the register allocation targets
 #endif
@@ -1721,18 +1706,16 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
         const uint32_t up = row[-3 * (FT_IN_P / 4)], dn = row[3 * (FT_IN_P / 4)];
         const uint32_t a4 = __builtin_amdgcn_alignbyte(rg, cc, 3);   // x+3 .. x+6
         const uint32_t a12 = __builtin_amdgcn_alignbyte(cc, lf, 1);  // x-3 .. x
-        const uint32_t mask = KL_SKIP_FAST ? 0u : compass4(cc, dn, a4, up, a12, tt) & colMask;
+        const uint32_t mask = compass4(cc, dn, a4, up, a12, tt) & colMask;
         if (qn > FT_Q - 64) {
-            if (!KL_SKIP_QUEUE) drain(qn);
+            drain(qn);
             qn = 0;
         }
         push(mask, rt, lane + 1);
     }
     KF_T(2);
-    if (!KL_SKIP_QUEUE) {
-        drain(qn);
-        if (np) strength_pass(0, np);  // the remainder, < 64 pixels
-    }
+    drain(qn);
+    if (np) strength_pass(0, np);  // the remainder, < 64 pixels
     KF_T(3);
     __syncthreads();
     KF_T(4);
@@ -1794,7 +1777,7 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
             const int c = (int)__umulhi((uint32_t)(Y - EDGE), (uint32_t)lg.cellHm) * lg.cols +
                           (int)__umulhi((uint32_t)(X - EDGE), (uint32_t)lg.cellWm);
             const int S = s_S[(rt + 1) * FT_SPW + ct + 4];
-            const int pos = KF_NOATOMIC ? k : atomicAdd(fcount + c, 1);
+            const int pos = atomicAdd(fcount + c, 1);
             if (pos < lg.capMax)
                 fcand[c * lg.capMax + pos] = ((uint32_t)(S - 1) << 24) | ((uint32_t)Y << 12) | (uint32_t)X;
         }
@@ -2137,22 +2120,17 @@ struct MatchGeom {
 //            best = first candidate with vMatchedDistance > dist, second = the next such;
 //            if a truncated top-8 holds < 2 such candidates the wave rescans the window.
 //   phase 3  rotation histogram, ComputeThreeMaxima, vnMatches12 / vbPrevMatched out.
-// Two instantiations of the same body:
-//   k_match_init      every per-slot array in LDS (<= 1024 octave-0 keypoints per frame);
-//                     a pair with more leaves nmOut[p] = -2 for the fallback
-//   k_match_init_big  the fallback (reference init extractor at 1280x720: nFeatures*2 = 5000,
-//                     Tracking.cc:126/217, ~1086 level-0 keypoints): only the greedy state
-//                     (vMatchedDistance / vnMatches21, vnMatches12, bins) stays in LDS, the
-//                     staged descriptors / coordinates / top-8 lists live in a per-workgroup
-//                     global scratch slot (L2-resident); up to 8192 keypoints per frame.
+// Two instantiations of the same body, both run by k_match_init's workgroup of a pair:
+//   <false>  every per-slot array in LDS (nmax octave-0 keypoints per frame, nmax <= 1024 by
+//            the batch size, see orb_search_for_initialization_batch_device); a pair with more
+//            returns true and is redone by
+//   <true>   the large-capacity body (e.g. the reference init extractor at 1280x720:
+//            nFeatures*2 = 5000, Tracking.cc:126/217, ~1086 level-0 keypoints): only the greedy
+//            state (vMatchedDistance / vnMatches21, vnMatches12, bins) stays in LDS, the staged
+//            descriptors / coordinates / top-8 lists live in the pair's global scratch slot
+//            (L2-resident); up to 8192 keypoints per frame.
 #define MATCH_TOPK 8
 #define MATCH_BIG_NMAX 8192
-#ifndef KM_SKIP1  // timing experiments only (wrong output): skip the phase-1 scan / phase 2
-#define KM_SKIP1 0
-#endif
-#ifndef KM_SKIP2
-#define KM_SKIP2 0
-#endif
 __device__ __forceinline__ void topk_insert(uint32_t (&t)[MATCH_TOPK], uint32_t key) {
 #pragma unroll
     for (int i = 0; i < MATCH_TOPK; ++i) {
@@ -2179,7 +2157,7 @@ struct MatchArgs {
     int P;
 };
 
-// Byte size of one k_match_init_big global scratch slot (nmax slots / queries).
+// Byte size of one global scratch slot of the large-capacity body (nmax slots / queries).
 __host__ __device__ inline size_t match_big_slot_bytes(int cap, int nmax) {
     // d2 32 + x2,y2,a2,cell 16 per F2 slot; q2i,qx,qy,lcnt 16 per query; top-8 lists
     // (also phase 0's key scratch: max(cap, 8 nmax) u32)
@@ -2187,8 +2165,9 @@ __host__ __device__ inline size_t match_big_slot_bytes(int cap, int nmax) {
     return ((size_t)nmax * 64 + keys * 4 + 255) & ~(size_t)255;
 }
 
+// Returns true (block-uniform) when the pair exceeded nmax and was left at -2 (-1 for BIG).
 template <bool BIG>
-__device__ __forceinline__ void match_pair(const MatchArgs& A, int p, uint8_t* __restrict__ smem,
+__device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, uint8_t* __restrict__ smem,
                                            uint8_t* __restrict__ gs) {
     constexpr int KB = BIG ? 13 : 11;  // slot bits of a (distance, slot) key
     constexpr uint32_t SLOT = (1u << KB) - 1u;
@@ -2197,7 +2176,7 @@ __device__ __forceinline__ void match_pair(const MatchArgs& A, int p, uint8_t* _
     __shared__ int s_ind[3];
     __shared__ int s_col[65];  // first slot of grid column cx (slots are in (cx, cy, index) order)
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int cap = A.cap, nmax = A.nmax;
+    const int cap = A.cap;
     const MatchGeom mg = A.mg;
     const float r = A.r, nnratio = A.nnratio;
     float* __restrict__ prev = A.prev;
@@ -2285,7 +2264,7 @@ __device__ __forceinline__ void match_pair(const MatchArgs& A, int p, uint8_t* _
     const int n2c = s_n2c, n1c = s_n1c;
     if (n2c > nmax || n1c > nmax) {  // capacity exceeded: fall back / report, never truncate silently
         if (tid == 0) A.nmOut[p] = BIG ? -1 : -2;
-        return;
+        return true;
     }
     // rank F2 candidates by traversal key -> slot
     for (int t = tid; t < n2c; t += 256) {
@@ -2349,7 +2328,7 @@ __device__ __forceinline__ void match_pair(const MatchArgs& A, int p, uint8_t* _
         for (int k = 0; k < MATCH_TOPK; ++k) top[k] = 0xFFFFFFFFu;
         int cnt = 0;
         // the window's grid columns only (an empty column range gives j0 >= j1)
-        const int j0 = s_col[min(minCX, 64)], j1 = KM_SKIP1 ? 0 : s_col[max(maxCX + 1, 0)];
+        const int j0 = s_col[min(minCX, 64)], j1 = s_col[max(maxCX + 1, 0)];
         for (int j = j0; j < j1; ++j) {
             const int cell = s_cell[j];
             const int cx = cell / 48, cy = cell - cx * 48;
@@ -2371,7 +2350,7 @@ __device__ __forceinline__ void match_pair(const MatchArgs& A, int p, uint8_t* _
     // Per query the critical path is one LDS read of its top-8 slots' state and scalar lane
     // reads (v_readlane: no LDS round trip); the next query's list is fetched while this one
     // resolves, and the rotation bins are computed afterwards, in parallel (phase 3).
-    if (wave == 0 && n1c > 0 && !KM_SKIP2) {
+    if (wave == 0 && n1c > 0) {
         int cntN = s_lcnt[0], i1N = s_q2i[0];
         uint32_t eN = lane < MATCH_TOPK ? s_list[lane] : 0xFFFFFFFFu;
         for (int q = 0; q < n1c; ++q) {
@@ -2527,23 +2506,20 @@ __device__ __forceinline__ void match_pair(const MatchArgs& A, int p, uint8_t* _
     if (lane == 0) s_hist[wave] = nm;
     __syncthreads();
     if (tid == 0) A.nmOut[p] = s_hist[0] + s_hist[1] + s_hist[2] + s_hist[3];
-    __syncthreads();  // s_hist / s_n*c are reused by the next pair of a big workgroup
+    return false;
 }
 
-__global__ void __launch_bounds__(256) k_match_init(MatchArgs A) {
+// One workgroup per pair.  A pair whose F1 queries or F2 candidates exceed the LDS capacity
+// A.nmax is redone in the same workgroup by the large-capacity body (nmaxBig, up to 8192
+// keypoints), its staged arrays in the pair's own slot of the global scratch `big` (null when
+// cap <= A.nmax: nothing can overflow).  The dynamic LDS covers both bodies' needs, so no
+// second launch and nothing per call beyond this kernel.
+__global__ void __launch_bounds__(256) k_match_init(MatchArgs A, uint8_t* __restrict__ big, int nmaxBig) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    match_pair<false>(A, blockIdx.x, smem, nullptr);
-}
-
-// The fallback over the pairs k_match_init left at -2: workgroup g owns global scratch slot g
-// and walks pairs g, g + gridDim.x, ... (grid <= P; a pair that fits exits at once).
-__global__ void __launch_bounds__(256) k_match_init_big(MatchArgs A, uint8_t* __restrict__ scratch) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint8_t* gs = scratch + (size_t)blockIdx.x * match_big_slot_bytes(A.cap, A.nmax);
-    for (int p = blockIdx.x; p < A.P; p += gridDim.x) {
-        if (A.nmOut[p] != -2) continue;  // block-uniform
-        __syncthreads();
-        match_pair<true>(A, p, smem, gs);
+    const int p = blockIdx.x;
+    if (match_pair<false>(A, p, A.nmax, smem, nullptr) && big) {
+        __syncthreads();  // the static LDS (counts, bins) is reused
+        match_pair<true>(A, p, nmaxBig, smem, big + (size_t)p * match_big_slot_bytes(A.cap, nmaxBig));
     }
 }
 
@@ -3416,7 +3392,7 @@ struct orb_extractor {
         // pre-filtered re-run, apart is faster at every measured size (B = 512, re-run + select:
         // 640x480 0.190 vs 0.239 ms inside; 1241x376 0.497 vs 0.696; 1280x720 0.864 vs 1.421).
         const bool sep = (B < KS_SEP_BATCH || (long long)W * H > KS_SEP_PIXELS) && cellLds;
-        if (sep && !KS_SKIP_RERUN) {
+        if (sep) {
             const int NWG = std::min(32, std::max(KR_NWG_MIN, 512 / (B * nlevels)));
             hipLaunchKernelGGL(k_rerun, dim3(B * NWG, nlevels), dim3(256), cellLds, st, d_pyr, d_cand, d_cellCount, g,
                                d_cells, NWG);
@@ -3720,6 +3696,34 @@ static size_t match_lds_bytes(int cap, int nmax) {
 }
 static size_t match_big_lds_bytes(int cap, int nmax) { return (size_t)nmax * 8 + (size_t)cap * 6 + 16; }
 
+// Global scratch of the large-capacity matcher body: one slot per pair, grow-only, one buffer per
+// (device, stream) so launches on one stream reuse it in stream order and concurrent streams
+// never share one.  Grown by a stream-ordered free + allocation on that stream; steady state:
+// no allocator call.  Only the slots of pairs that overflow the LDS capacity are ever touched.
+static std::mutex g_bigMu;
+static std::vector<std::pair<std::pair<int, hipStream_t>, std::pair<void*, size_t>>> g_big;
+static int match_big_scratch(hipStream_t st, size_t bytes, void** out) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(g_bigMu);
+    for (auto& e : g_big)
+        if (e.first.first == dev && e.first.second == st) {
+            if (e.second.second < bytes) {
+                HIP_TRY(hipFreeAsync(e.second.first, st));
+                e.second = {nullptr, 0};
+                HIP_TRY(hipMallocAsync(&e.second.first, bytes, st));
+                e.second.second = bytes;
+            }
+            *out = e.second.first;
+            return ORB_OK;
+        }
+    void* p = nullptr;
+    HIP_TRY(hipMallocAsync(&p, bytes, st));
+    g_big.push_back({{dev, st}, {p, bytes}});
+    *out = p;
+    return ORB_OK;
+}
+
 int orb_search_for_initialization_batch_device(const orb_keypoint_t* d_kps, const uint8_t* d_desc,
                                                const int32_t* d_counts, int cap, int P, const int32_t* d_pair_f1,
                                                const int32_t* d_pair_f2, orb_frame_bounds_t bounds, float nnratio,
@@ -3736,21 +3740,19 @@ int orb_search_for_initialization_batch_device(const orb_keypoint_t* d_kps, cons
     // fill the chip, 0.225 of the capacity covers its output and leaves room for two or more
     // work-groups per CU (640x480: 0.233 -> 0.129 ms for 511 pairs, 1241x376: 0.47 -> 0.26);
     // any frame beyond (another producer, another scale factor) is redone exactly by
-    // k_match_init_big below.  Fewer pairs than CUs: one work-group per CU anyway, and the
-    // full capacity spares the per-frame path the fallback launch.
+    // the large-capacity body in the same workgroup.  Fewer pairs than CUs: one work-group per CU anyway, and the
+    // full capacity spares the per-frame path the fallback scratch.
     const int nmax = P < 256 ? std::min(cap, 1024)
                              : std::min({cap, 1024, std::max(MATCH_NMAX_MIN,
                                                              (int)(((long long)cap * MATCH_NMAX_NUM / 40 + 31) & ~31))});
-    const size_t lds = match_lds_bytes(cap, nmax);
     const int nmaxBig = std::min(cap, MATCH_BIG_NMAX);
-    const size_t ldsBig = match_big_lds_bytes(cap, nmaxBig);
-    if (lds > 159 * 1024 || ldsBig > 159 * 1024)  // 160 KB per CU minus the kernels' static LDS
+    // the large-capacity body runs in the same workgroup: the dynamic LDS covers both
+    const size_t lds = std::max(match_lds_bytes(cap, nmax), cap > nmax ? match_big_lds_bytes(cap, nmaxBig) : 0);
+    if (lds > 159 * 1024)  // 160 KB per CU minus the kernel's static LDS
         return set_err(ORB_ENOTSUP, "per-frame keypoint capacity too large for LDS");
     static std::once_flag attrOnce;
     std::call_once(attrOnce, [] {
         (void)hipFuncSetAttribute((const void*)k_match_init, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
-        (void)hipFuncSetAttribute((const void*)k_match_init_big, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  159 * 1024);
         (void)hipGetLastError();  // an unsupported attribute value must not surface as the launch's error
     });
     MatchGeom mg{bounds.min_x, bounds.max_x, bounds.min_y, bounds.max_y,
@@ -3759,22 +3761,11 @@ int orb_search_for_initialization_batch_device(const orb_keypoint_t* d_kps, cons
     MatchArgs A{d_kps, d_desc, d_counts, cap, nmax, d_pair_f1, d_pair_f2, mg, nnratio, check_ori, (float)window,
                 d_prev_xy, d_matches12, d_nmatches, P};
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_match_init, dim3(P), dim3(256), lds, st, A);
+    void* big = nullptr;
+    if (cap > nmax)  // a pair may overflow the LDS capacity: its slot of the large-capacity scratch
+        if (int r = match_big_scratch(st, match_big_slot_bytes(cap, nmaxBig) * (size_t)P, &big)) return r;
+    hipLaunchKernelGGL(k_match_init, dim3(P), dim3(256), lds, st, A, (uint8_t*)big, nmaxBig);
     HIP_TRY(hipGetLastError());
-    if (cap > nmax) {
-        // pairs with more than 1024 octave-0 keypoints in a frame (k_match_init left -2) are
-        // redone by the large-capacity kernel; its scratch is stream-ordered
-        const int G = std::min(P, 256);
-        const size_t slot = match_big_slot_bytes(cap, nmaxBig);
-        void* scratch = nullptr;
-        HIP_TRY(hipMallocAsync(&scratch, slot * G, st));
-        A.nmax = nmaxBig;
-        hipLaunchKernelGGL(k_match_init_big, dim3(G), dim3(256), ldsBig, st, A, (uint8_t*)scratch);
-        hipError_t e = hipGetLastError();
-        hipError_t f = hipFreeAsync(scratch, st);
-        if (e != hipSuccess) return set_err(ORB_EDEVICE, std::string("k_match_init_big: ") + hipGetErrorString(e));
-        if (f != hipSuccess) return set_err(ORB_EDEVICE, std::string("hipFreeAsync: ") + hipGetErrorString(f));
-    }
     return ORB_OK;
 }
 
@@ -3985,13 +3976,6 @@ int orb_debug_kf_timing(unsigned long long* out6) {
     return ORB_OK;
 }
 #endif
-// Retired k_level queue statistics hook (the FAST queue of k_fast is not instrumented): zeros.
-int orb_debug_klevel_counts(unsigned long long* out3) {
-    if (!out3) return set_err(ORB_EINVAL, "bad arguments");
-    out3[0] = out3[1] = out3[2] = 0;
-    return ORB_OK;
-}
-
 int orb_debug_cell_counts(orb_extractor_t* h, int b, int l, int* counts, int cap) {
     if (!h || l < 0 || l >= h->nlevels || !h->d_cellCount) return set_err(ORB_EINVAL, "bad arguments");
     const LevelGeom& lg = h->g.lv[l];

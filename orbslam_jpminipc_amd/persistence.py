@@ -17,6 +17,7 @@ streams without a host round trip per keyframe.
 from __future__ import annotations
 
 import ctypes
+import struct
 
 import numpy as np
 
@@ -57,7 +58,9 @@ def read_keypoint_record(data, offset: int = 0):
     b = np.ascontiguousarray(_buf(data, offset))
     n, used, ok = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_int()
     L = hip_lib()
-    cap = (b.size - 10) // 28 if b.size >= 10 else 0
+    # the record's own count (u64 after the 2-byte header), bounded by what the buffer can hold:
+    # the output is sized to this record, not to the rest of the stream
+    cap = min(struct.unpack_from("<Q", b, 2)[0], (b.size - 10) // 28) if b.size >= 10 else 0
     k = np.empty(max(cap, 1), KEYPOINT_DTYPE)
     check(L.orb_read_keypoint_record(ptr(b), b.size, ptr(k), cap, ctypes.byref(n), ctypes.byref(used),
                                      ctypes.byref(ok)))
@@ -67,7 +70,7 @@ def read_keypoint_record(data, offset: int = 0):
 def read_descriptor_record(data, offset: int = 0):
     """-> (descriptors (n, 32) uint8, bytes consumed, header_ok) of the record at `offset`."""
     b = np.ascontiguousarray(_buf(data, offset))
-    cap = (b.size - 6) // 32 if b.size >= 6 else 0
+    cap = max(min(struct.unpack_from("<i", b, 2)[0], (b.size - 6) // 32), 0) if b.size >= 6 else 0
     d = np.empty((max(cap, 1), 32), np.uint8)
     n, used, ok = ctypes.c_int(), ctypes.c_size_t(), ctypes.c_int()
     check(hip_lib().orb_read_descriptor_record(ptr(b), b.size, ptr(d), cap, ctypes.byref(n), ctypes.byref(used),

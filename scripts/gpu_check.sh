@@ -1,6 +1,6 @@
 #!/bin/bash
 # Quick GPU session: parity tests, bench, per-stage times of the in-tree build and of the
-# ablation variants in build/variants (scripts/klevel_phases.sh, scripts/build_variant.sh).
+# ablation variants in build/variants (scripts/build_variant.sh).
 # Usage (via gpurun): bash scripts/gpu_check.sh TAG
 set -o pipefail
 TAG=${1:-check}

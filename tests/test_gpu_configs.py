@@ -19,10 +19,21 @@ from oracle_lib import Oracle, OracleMatcher, search_for_initialization
 pytestmark = pytest.mark.gpu
 
 
-def _oracle_extract_all(frames, nf, threads=8):
+def _oracle_threads():
+    import os
+
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))  # the GPU box's CPU share is 16
+
+
+def _oracle_extract_all(frames, nf, threads=None):
     """Oracle extraction of every frame, `threads` oracle instances in parallel (ctypes
     releases the GIL)."""
     out = [None] * len(frames)
+    threads = threads or _oracle_threads()
 
     def work(t):
         ora = Oracle(nf, 1.2, 8, 1, 20)
@@ -37,20 +48,25 @@ def _oracle_extract_all(frames, nf, threads=8):
     return out
 
 
-def _device_extract_and_match(frames, nf):
+def _device_extract_and_match(frames, nf, pairs=None):
+    """bench.py's step on `frames`: orb_extract_batch_device, then the batched
+    SearchForInitialization over `pairs` (default: every consecutive pair)."""
     import torch
 
     B, H, W = frames.shape
     ext = orb.ORBextractor(nf, 1.2, 8, orb.FAST_SCORE, 20, device=0, max_batch=B)
     d = torch.from_numpy(frames).cuda()
     kps, desc, cnt = ext.extract_batch_device(d)
-    f1 = torch.arange(0, B - 1, dtype=torch.int32, device="cuda")
-    m12, nm = orb.ORBmatcher(0.9, True).search_for_initialization_batch_device(kps, desc, cnt, f1, f1 + 1, W, H, 100)
+    if pairs is None:
+        pairs = [(b, b + 1) for b in range(B - 1)]
+    f1 = torch.tensor([a for a, _ in pairs], dtype=torch.int32, device="cuda")
+    f2 = torch.tensor([b for _, b in pairs], dtype=torch.int32, device="cuda")
+    m12, nm = orb.ORBmatcher(0.9, True).search_for_initialization_batch_device(kps, desc, cnt, f1, f2, W, H, 100)
     torch.cuda.synchronize()
     return kps.cpu().numpy(), desc.cpu().numpy(), cnt.cpu().numpy(), m12.cpu().numpy(), nm.cpu().numpy()
 
 
-def _check_batch(frames, nf, kps, desc, cnt, m12, nm):
+def _check_batch(frames, nf, kps, desc, cnt, m12, nm, pairs=None):
     B, H, W = frames.shape
     ref = _oracle_extract_all(frames, nf)
     for b in range(B):
@@ -58,13 +74,23 @@ def _check_batch(frames, nf, kps, desc, cnt, m12, nm):
         assert cnt[b] == len(ko), b
         assert kps[b, : cnt[b]].tobytes() == ko.tobytes(), f"frame {b} keypoints"
         assert desc[b, : cnt[b]].tobytes() == do.tobytes(), f"frame {b} descriptors"
-    for p in range(B - 1):
-        k1, d1 = ref[p]
-        k2, d2 = ref[p + 1]
+    if pairs is None:
+        pairs = [(b, b + 1) for b in range(B - 1)]
+    for p, (a, b) in enumerate(pairs):
+        k1, d1 = ref[a]
+        k2, d2 = ref[b]
         prev = np.ascontiguousarray(np.stack([k1["x"], k1["y"]], 1).astype(np.float32))
         no, m12o = search_for_initialization(k1, d1, k2, d2, W, H, prev, 0.9, True, 100)
         assert nm[p] == no, p
-        assert np.array_equal(m12[p, : cnt[p]], m12o), p
+        assert np.array_equal(m12[p, : cnt[a]], m12o), p
+
+
+def _bench_stream_batch(W, H, streams, per):
+    """bench.py's frames and pairs for `streams` camera streams of `per` frames each (c5 at
+    N ranks: rank r owns streams r, r + N, ...; c3 / c4: one stream = the rank)."""
+    frames = np.concatenate([orb.synth_stream(W, H, stream=s, first=0, count=per) for s in streams])
+    pairs = [(k * per + t, k * per + t + 1) for k in range(len(streams)) for t in range(per - 1)]
+    return frames, pairs
 
 
 def test_bench_batch_full_parity():
@@ -72,6 +98,31 @@ def test_bench_batch_full_parity():
     0, first 0, count 512)): all 512 frames and all 511 pairs bit-exact."""
     frames = orb.synth_stream(640, 480, stream=0, first=0, count=512)
     _check_batch(frames, 1000, *_device_extract_and_match(frames, 1000))
+
+
+def test_bench_batch_c4_full_parity():
+    """bench.py --workload c4's timed batch: 512 KITTI-shaped 1241x376 frames of stream 0,
+    ORBextractor(2000, 1.2, 8), 511 consecutive pairs.  Exercises k_rerun at its large-batch
+    workgroup count and k_match_init's reduced LDS capacity (P >= 256) at this geometry: every
+    frame and every pair bit-exact."""
+    frames, pairs = _bench_stream_batch(1241, 376, [0], 512)
+    _check_batch(frames, 2000, *_device_extract_and_match(frames, 2000, pairs), pairs=pairs)
+
+
+def test_bench_batch_c5_full_parity():
+    """bench.py --workload c5's timed batch at N = 1: 8 independent 1280x720 streams x 128
+    frames (B = 1024), ORBextractor(2500, 1.2, 8), the 8 x 127 within-stream pairs: every frame
+    and every pair bit-exact."""
+    frames, pairs = _bench_stream_batch(1280, 720, range(8), 128)
+    _check_batch(frames, 2500, *_device_extract_and_match(frames, 2500, pairs), pairs=pairs)
+
+
+@pytest.mark.parametrize("rank", [3])
+def test_bench_batch_c5_rank_of_eight_parity(rank):
+    """c5 at N = 8: one rank's load is one stream of 128 frames (B = 128, 127 pairs), below the
+    pyramid-stream and reduced-capacity matcher thresholds: bit-exact."""
+    frames, pairs = _bench_stream_batch(1280, 720, [rank], 128)
+    _check_batch(frames, 2500, *_device_extract_and_match(frames, 2500, pairs), pairs=pairs)
 
 
 def test_match_batch_device_over_lds_capacity():
