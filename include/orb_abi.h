@@ -294,6 +294,27 @@ int orb_search_by_sim3(const orb_frame_view_t* KF1, orb_map_points_t mp1, const 
 int orb_fuse(const orb_frame_view_t* KF, orb_map_points_t pts, const uint8_t* usable, float th, int scw,
              int32_t* best_idx, int* n_fused, int device);
 
+/* ---- Frame keypoint geometry (GPU: csrc/orb_frame.hip) ------------------------------ */
+/* The camera as Tracking.cc:52-70 builds it: K4 = (fx, fy, cx, cy) of K = [fx 0 cx; 0 fy cy;
+ * 0 0 1], dist4 = mDistCoef = (k1, k2, p1, p2).  cv::undistortPoints(pts, pts, K, mDistCoef,
+ * noArray(), K) (OpenCV 2.4 cvUndistortPoints: double arithmetic, 5 fixed iterations) is
+ * restated exactly on the device.  fx, fy must be finite and non-zero (ORB_EINVAL). */
+/* Frame::UndistortKeyPoints (Frame.cc:289-319) over a [B][cap] extractor batch: slot i < counts[b]
+ * of d_kps_un = that keypoint with pt undistorted, or copied unchanged when k1 == 0
+ * (Frame.cc:291-295).  d_kps_un may equal d_kps.  Asynchronous on `stream`. */
+int orb_undistort_keypoints_batch_device(const orb_keypoint_t* d_kps, const int32_t* d_counts, int cap, int B,
+                                         const float* K4, const float* dist4, orb_keypoint_t* d_kps_un,
+                                         void* stream);
+/* The same for one frame's n keypoints in host buffers (synchronous; device -1 = current). */
+int orb_undistort_keypoints(const orb_keypoint_t* kps, int n, const float* K4, const float* dist4, int device,
+                            orb_keypoint_t* out);
+/* cv::undistortPoints itself on n points xy[2n] -> out[2n] (no k1 == 0 shortcut). */
+int orb_undistort_points(const float* xy, int n, const float* K4, const float* dist4, int device, float* out);
+/* Frame::ComputeImageBounds (Frame.cc:321-349): the undistorted image corners' floor / ceil
+ * when k1 != 0, else the image rectangle. */
+int orb_compute_image_bounds(int cols, int rows, const float* K4, const float* dist4, int device,
+                             orb_frame_bounds_t* out);
+
 /* ---- the front end over a camera stream, overlapped (csrc/orb_pipeline.hip) ---------- */
 /* B consecutive frames of one camera: ORBextractor::operator() on each (Frame::Frame,
  * Frame.cc:56-128) and SearchForInitialization(F_b, F_b+1) for b < B-1 with vbPrevMatched =
@@ -314,6 +335,17 @@ int orb_pipeline_extract_and_match(orb_pipeline_t* p, int B, const uint8_t* d_im
                                    int64_t frame_pitch, orb_keypoint_t* d_kps, uint8_t* d_desc, int32_t* d_counts,
                                    orb_frame_bounds_t bounds, float nnratio, int check_ori, int window,
                                    int32_t* d_matches12, int32_t* d_nmatches, void* stream);
+/* The same step for a calibrated camera with distortion (Frame::Frame: UndistortKeyPoints,
+ * Frame.cc:69): after each chunk's extraction its keypoints are undistorted into d_kps_un
+ * (orb_undistort_keypoints_batch_device; K4 / dist4 as there) and the pairs are matched on
+ * mvKeysUn, with `bounds` = orb_compute_image_bounds of the camera.  K4 = NULL is
+ * orb_pipeline_extract_and_match (d_kps_un unused). */
+int orb_pipeline_extract_undistort_and_match(orb_pipeline_t* p, int B, const uint8_t* d_imgs, int w, int hgt,
+                                             int stride, int64_t frame_pitch, const float* K4, const float* dist4,
+                                             orb_keypoint_t* d_kps, orb_keypoint_t* d_kps_un, uint8_t* d_desc,
+                                             int32_t* d_counts, orb_frame_bounds_t bounds, float nnratio,
+                                             int check_ori, int window, int32_t* d_matches12, int32_t* d_nmatches,
+                                             void* stream);
 /* Per-stage HIP-event timing summed over the chunk handles (see orb_profile_*). */
 int orb_pipeline_profile_enable(orb_pipeline_t* p, int enable);
 int orb_pipeline_profile_read(orb_pipeline_t* p, double* stage_ms, int64_t* stage_launches, int nstages);

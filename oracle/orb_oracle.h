@@ -120,6 +120,14 @@ int oracle_search_for_triangulation(const orb_frame_view_t* KF1, const uint8_t* 
                                     const float* F12, float nnratio, int check_ori, int32_t* match12,
                                     int* n_matches);
 
+/* ---- orb_oracle_frame.cpp: Frame::UndistortKeyPoints / ComputeImageBounds (Frame.cc:289-349),
+ * cv::undistortPoints (OpenCV 2.4 cvUndistortPoints) restated.  K4 = (fx, fy, cx, cy),
+ * dist4 = (k1, k2, p1, p2). ---------------------------------------------------------------- */
+int oracle_undistort_points(const float* K4, const float* dist4, const float* xy, int n, float* out);
+int oracle_undistort_keypoints(const orb_keypoint_t* kps, int n, const float* K4, const float* dist4,
+                               orb_keypoint_t* out);
+int oracle_compute_image_bounds(int cols, int rows, const float* K4, const float* dist4, orb_frame_bounds_t* b);
+
 /* ---- orb_oracle_color.cpp: cvtColor(CV_RGB2GRAY / CV_BGR2GRAY) 8U (Tracking.cc:202-207) ---- */
 int oracle_rgb_to_gray(const uint8_t* src, int w, int h, int stride, int cn, int rgb, uint8_t* dst);
 

@@ -149,6 +149,14 @@ HIP_SIGNATURES = {
         _i,
         [_vp, _i, _vp, _i, _i, _i, _i64, _vp, _vp, _vp, FrameBounds, _f, _i, _i, _vp, _vp, _vp],
     ),
+    "orb_pipeline_extract_undistort_and_match": (
+        _i,
+        [_vp, _i, _vp, _i, _i, _i, _i64, _vp, _vp, _vp, _vp, _vp, _vp, FrameBounds, _f, _i, _i, _vp, _vp, _vp],
+    ),
+    "orb_undistort_keypoints_batch_device": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp, _vp]),
+    "orb_undistort_keypoints": (_i, [_vp, _i, _vp, _vp, _i, _vp]),
+    "orb_undistort_points": (_i, [_vp, _i, _vp, _vp, _i, _vp]),
+    "orb_compute_image_bounds": (_i, [_i, _i, _vp, _vp, _i, ctypes.POINTER(FrameBounds)]),
     "orb_pipeline_profile_enable": (_i, [_vp, _i]),
     "orb_pipeline_profile_read": (_i, [_vp, _vp, _vp, _i]),
     "orb_compute_distinctive_descriptors": (_i, [_i, _vp, _vp, _vp, _vp, _vp, _i]),

@@ -2131,6 +2131,15 @@ struct MatchGeom {
 //            (L2-resident); up to 8192 keypoints per frame.
 #define MATCH_TOPK 8
 #define MATCH_BIG_NMAX 8192
+#ifndef KM_TIMING  // 1: per-phase s_memrealtime sums of k_match_init's pairs (experiment builds only)
+#define KM_TIMING 0
+#endif
+#if KM_TIMING
+__device__ unsigned long long g_kmtime[8];
+#define KM_T(i) const unsigned long long kmt##i = __builtin_amdgcn_s_memrealtime()
+#else
+#define KM_T(i)
+#endif
 __device__ __forceinline__ void topk_insert(uint32_t (&t)[MATCH_TOPK], uint32_t key) {
 #pragma unroll
     for (int i = 0; i < MATCH_TOPK; ++i) {
@@ -2224,6 +2233,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
         s_list = (uint32_t*)(s_lcnt + nmax);
     }
     uint32_t* s_key = s_list;  // phase-0 scratch (cap entries)
+    KM_T(0);
     const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     // ---- phase 0: keys in parallel, then ordered compaction ----
     // s_key[i2] = traversal key of F2 keypoint i2 or ~0 (not octave 0 / outside the grid);
@@ -2266,6 +2276,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
         if (tid == 0) A.nmOut[p] = BIG ? -1 : -2;
         return true;
     }
+    KM_T(1);
     // rank F2 candidates by traversal key -> slot
     for (int t = tid; t < n2c; t += 256) {
         const uint32_t k = s_key[t];
@@ -2305,6 +2316,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
         s_col[tid] = lo;
     }
     __syncthreads();
+    KM_T(2);
     // ---- phase 1: per-query top-8 (dist, order) ----
     for (int q0 = 0; q0 < n1c; q0 += 256) {
         const int q = q0 + tid;
@@ -2346,6 +2358,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
     }
     if constexpr (BIG) __threadfence_block();
     __syncthreads();
+    KM_T(3);
     // ---- phase 2: the sequential greedy pass (ORBmatcher.cc:611-680) on one wave ----
     // Per query the critical path is one LDS read of its top-8 slots' state and scalar lane
     // reads (v_readlane: no LDS round trip); the next query's list is fetched while this one
@@ -2434,6 +2447,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
         }
     }
     __syncthreads();
+    KM_T(4);
     // ---- phase 3 ----
     if (A.checkOri) {
         if (tid < 32) s_hist[tid] = 0;
@@ -2506,6 +2520,19 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
     if (lane == 0) s_hist[wave] = nm;
     __syncthreads();
     if (tid == 0) A.nmOut[p] = s_hist[0] + s_hist[1] + s_hist[2] + s_hist[3];
+#if KM_TIMING
+    KM_T(5);
+    if (tid == 0 && !BIG) {
+        atomicAdd(&g_kmtime[0], kmt1 - kmt0);  // phase 0: keys + compaction
+        atomicAdd(&g_kmtime[1], kmt2 - kmt1);  // ranking + staging
+        atomicAdd(&g_kmtime[2], kmt3 - kmt2);  // phase 1
+        atomicAdd(&g_kmtime[3], kmt4 - kmt3);  // phase 2
+        atomicAdd(&g_kmtime[4], kmt5 - kmt4);  // phase 3 + output
+        atomicAdd(&g_kmtime[5], 1ull);
+        atomicAdd(&g_kmtime[6], (unsigned long long)n1c);
+        atomicAdd(&g_kmtime[7], (unsigned long long)n2c);
+    }
+#endif
     return false;
 }
 
@@ -3962,6 +3989,17 @@ extern "C" int orb_debug_ps_timing(unsigned long long* out6) {
     HIP_TRY(hipMemcpyFromSymbol(out6, HIP_SYMBOL(g_pstime), 32 * sizeof(unsigned long long)));
     unsigned long long z[32] = {};
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_pstime), z, sizeof(z)));
+    return ORB_OK;
+}
+#endif
+#if KM_TIMING
+// experiment builds: k_match_init's per-phase s_memrealtime (100 MHz) sums
+// {phase 0, rank, phase 1, phase 2, phase 3, pairs, queries, candidates}
+extern "C" int orb_debug_km_timing(unsigned long long* out8) {
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_kmtime), 8 * sizeof(unsigned long long)));
+    unsigned long long z[8] = {};
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_kmtime), z, sizeof(z)));
     return ORB_OK;
 }
 #endif

@@ -116,8 +116,21 @@ int orb_pipeline_extract_and_match(orb_pipeline_t* p, int B, const uint8_t* d_im
                                    int64_t frame_pitch, orb_keypoint_t* d_kps, uint8_t* d_desc, int32_t* d_counts,
                                    orb_frame_bounds_t bounds, float nnratio, int check_ori, int window,
                                    int32_t* d_matches12, int32_t* d_nmatches, void* stream) {
+    return orb_pipeline_extract_undistort_and_match(p, B, d_imgs, w, hgt, stride, frame_pitch, nullptr, nullptr, d_kps,
+                                                    nullptr, d_desc, d_counts, bounds, nnratio, check_ori, window,
+                                                    d_matches12, d_nmatches, stream);
+}
+
+int orb_pipeline_extract_undistort_and_match(orb_pipeline_t* p, int B, const uint8_t* d_imgs, int w, int hgt,
+                                             int stride, int64_t frame_pitch, const float* K4, const float* dist4,
+                                             orb_keypoint_t* d_kps, orb_keypoint_t* d_kps_un, uint8_t* d_desc,
+                                             int32_t* d_counts, orb_frame_bounds_t bounds, float nnratio,
+                                             int check_ori, int window, int32_t* d_matches12, int32_t* d_nmatches,
+                                             void* stream) {
     if (!p || B <= 0 || !d_imgs || !d_kps || !d_desc || !d_counts || (B > 1 && (!d_matches12 || !d_nmatches)))
         return fail(ORB_EINVAL, "bad arguments");
+    const bool undistort = K4 != nullptr;
+    if (undistort && (!dist4 || !d_kps_un)) return fail(ORB_EINVAL, "camera given without coefficients / mvKeysUn");
     if (B > p->maxBatch) return fail(ORB_EINVAL, "B exceeds max_batch");
     PCHK(hipSetDevice(p->device));
     const hipStream_t caller = (hipStream_t)stream;
@@ -131,13 +144,18 @@ int orb_pipeline_extract_and_match(orb_pipeline_t* p, int B, const uint8_t* d_im
                                           frame_pitch, d_kps + (long long)b0 * cap, d_desc + (long long)b0 * cap * 32,
                                           d_counts + b0, s);
         if (st) return st;
+        // Frame::UndistortKeyPoints on the chunk's stream (Frame.cc:69, 289-319)
+        if (undistort && (st = orb_undistort_keypoints_batch_device(d_kps + (long long)b0 * cap, d_counts + b0, cap, n,
+                                                                    K4, dist4, d_kps_un + (long long)b0 * cap, s)))
+            return st;
         PCHK(hipEventRecord(p->extracted[c], s));
     }
     // every pair once the chunks are extracted, on the caller's stream: a matcher work-group
     // takes most of a CU's LDS, so matching beside the extraction slowed both (measured)
     for (int c = 0; c < S; ++c) PCHK(hipStreamWaitEvent(caller, p->extracted[c], 0));
     if (B > 1) {
-        int st = orb_search_for_initialization_batch_device(d_kps, d_desc, d_counts, cap, B - 1, p->d_iota,
+        int st = orb_search_for_initialization_batch_device(undistort ? d_kps_un : d_kps, d_desc, d_counts, cap, B - 1,
+                                                            p->d_iota,
                                                             p->d_iota + 1, bounds, nnratio, check_ori, window,
                                                             nullptr, d_matches12, d_nmatches, caller);
         if (st) return st;

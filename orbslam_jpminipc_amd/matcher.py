@@ -15,26 +15,37 @@ from .views import FeatureVector, MapPointSet, View, flags
 
 
 class Frame:
-    """The matcher-facing part of ORB_SLAM::Frame: mvKeysUn, mDescriptors, image bounds.
+    """The matcher-facing part of ORB_SLAM::Frame: mvKeys, mvKeysUn, mDescriptors, image bounds.
 
-    With zero distortion (k1 == 0, the configs' camera) mvKeysUn == mvKeys (Frame.cc:291-295)
-    and the grid bounds are the image rectangle (Frame.cc:343-347).
+    Without a camera, or with k1 == 0 (the configs' camera), mvKeysUn == mvKeys
+    (Frame.cc:291-295) and the grid bounds are the image rectangle (Frame.cc:343-347).  With
+    K and distCoef (k1, k2, p1, p2) and k1 != 0, mvKeysUn = UndistortKeyPoints (Frame.cc:297-318)
+    and the bounds ComputeImageBounds (Frame.cc:323-340), both on the GPU (camera.py).
     """
 
-    def __init__(self, keypoints: np.ndarray, descriptors, width: int, height: int):
+    def __init__(self, keypoints: np.ndarray, descriptors, width: int, height: int, K=None, distCoef=None):
         self.mvKeys = np.asarray(keypoints, KEYPOINT_DTYPE)
         self.mvKeysUn = self.mvKeys
         self.N = len(self.mvKeys)
         self.mDescriptors = (np.zeros((0, 32), np.uint8) if descriptors is None
                              else np.ascontiguousarray(descriptors, np.uint8))
         self.mnMinX, self.mnMaxX, self.mnMinY, self.mnMaxY = 0, int(width), 0, int(height)
+        if (K is None) != (distCoef is None):
+            raise ValueError("K and distCoef go together")
+        if K is not None:
+            from . import camera
+
+            if self.N:
+                self.mvKeysUn = camera.undistort_keypoints(self.mvKeys, K, distCoef)
+            b = camera.compute_image_bounds(width, height, K, distCoef)
+            self.mnMinX, self.mnMaxX, self.mnMinY, self.mnMaxY = b.min_x, b.max_x, b.min_y, b.max_y
 
     @classmethod
-    def from_image(cls, image: np.ndarray, extractor) -> "Frame":
+    def from_image(cls, image: np.ndarray, extractor, K=None, distCoef=None) -> "Frame":
         kps, desc = extractor(image)
         if kps is None:
             kps = np.zeros(0, KEYPOINT_DTYPE)
-        return cls(kps, desc, image.shape[1], image.shape[0])
+        return cls(kps, desc, image.shape[1], image.shape[0], K, distCoef)
 
     def bounds(self) -> FrameBounds:
         return FrameBounds(self.mnMinX, self.mnMaxX, self.mnMinY, self.mnMaxY)
@@ -245,11 +256,14 @@ class ORBmatcher:
         return [out[off[i]:off[i + 1]].copy() for i in range(q)]
 
     def search_for_initialization_batch_device(self, d_kps, d_desc, d_counts, pair_f1, pair_f2, width: int,
-                                               height: int, windowSize: int = 100, d_prev_xy=None, stream=None):
+                                               height: int, windowSize: int = 100, d_prev_xy=None, stream=None,
+                                               bounds=None):
         """Batched SearchForInitialization over device extractor output (one wave per pair).
 
         d_kps (B, cap, 28) / d_desc (B, cap, 32) / d_counts (B,) as returned by
-        ORBextractor.extract_batch_device; pair_f1 / pair_f2 int32 device tensors (P,).
+        ORBextractor.extract_batch_device (or mvKeysUn from camera.undistort_keypoints_batch_device,
+        with `bounds` = camera.compute_image_bounds; default: the image rectangle);
+        pair_f1 / pair_f2 int32 device tensors (P,).
         Returns (d_matches12 (P, cap) int32, d_nmatches (P,) int32).
         """
         import torch
@@ -262,6 +276,6 @@ class ORBmatcher:
         s = stream if stream is not None else torch.cuda.current_stream(dev)
         check(self._lib.orb_search_for_initialization_batch_device(
             ptr(d_kps), ptr(d_desc), ptr(d_counts), cap, P, ptr(pair_f1), ptr(pair_f2),
-            FrameBounds(0, width, 0, height), self.mfNNratio, int(self.mbCheckOrientation), int(windowSize),
+            bounds if bounds is not None else FrameBounds(0, width, 0, height), self.mfNNratio, int(self.mbCheckOrientation), int(windowSize),
             ptr(d_prev_xy), ptr(m12), ptr(nm), ctypes.c_void_p(s.cuda_stream)))
         return m12, nm

@@ -56,6 +56,9 @@ def lib() -> ctypes.CDLL:
         L.oracle_resize.argtypes = [vp, i, i, i, vp, i, i, i]
         L.oracle_blur_padded.argtypes = [vp, i, i, vp]
         L.oracle_fast.argtypes = [vp, i, i, i, i, vp, i]
+        L.oracle_undistort_points.argtypes = [vp, vp, vp, i, vp]
+        L.oracle_undistort_keypoints.argtypes = [vp, i, vp, vp, vp]
+        L.oracle_compute_image_bounds.argtypes = [i, i, vp, vp, ctypes.POINTER(_Bounds)]
         L.oracle_bench.restype = ctypes.c_double
         L.oracle_bench.argtypes = [i, f, i, i, vp, i, i, i, i, ctypes.c_int64, i, i, ctypes.POINTER(ctypes.c_int64),
                                    ctypes.POINTER(ctypes.c_int64)]
@@ -123,8 +126,10 @@ class Oracle:
         return search_for_initialization(k1, d1, k2, d2, width, height, prev, nnratio, checkOri, window)
 
 
-def search_for_initialization(k1, d1, k2, d2, width, height, prev, nnratio=0.9, checkOri=True, window=100):
-    """Oracle SearchForInitialization (ORBmatcher.cc:598-713); prev updated in place."""
+def search_for_initialization(k1, d1, k2, d2, width, height, prev, nnratio=0.9, checkOri=True, window=100,
+                              bounds=None):
+    """Oracle SearchForInitialization (ORBmatcher.cc:598-713); prev updated in place.  `bounds`
+    = (min_x, max_x, min_y, max_y) of the frame grid (default: the image rectangle)."""
     L = lib()
     k1 = np.ascontiguousarray(k1, KEYPOINT_DTYPE)
     k2 = np.ascontiguousarray(k2, KEYPOINT_DTYPE)
@@ -133,10 +138,34 @@ def search_for_initialization(k1, d1, k2, d2, width, height, prev, nnratio=0.9, 
     m12 = np.full(len(k1), -1, np.int32)
     n = ctypes.c_int()
     st = L.oracle_search_for_initialization(_p(k1), _p(d1), len(k1), _p(k2), _p(d2), len(k2),
-                                            _Bounds(0, width, 0, height), nnratio, int(checkOri), window, _p(prev),
+                                            _Bounds(*(bounds or (0, width, 0, height))), nnratio, int(checkOri), window, _p(prev),
                                             _p(m12), ctypes.byref(n))
     assert st == 0
     return n.value, m12
+
+
+# ---- Frame::UndistortKeyPoints / ComputeImageBounds (oracle/orb_oracle_frame.cpp) ----------
+def undistort_points(xy, K4, dist4):
+    xy = np.ascontiguousarray(np.asarray(xy, np.float32).reshape(-1, 2))
+    out = np.empty_like(xy)
+    k, d = np.ascontiguousarray(K4, np.float32), np.ascontiguousarray(dist4, np.float32)
+    assert lib().oracle_undistort_points(_p(k), _p(d), _p(xy), len(xy), _p(out)) == 0
+    return out
+
+
+def undistort_keypoints(kps, K4, dist4):
+    kps = np.ascontiguousarray(kps, KEYPOINT_DTYPE)
+    out = np.empty_like(kps)
+    k, d = np.ascontiguousarray(K4, np.float32), np.ascontiguousarray(dist4, np.float32)
+    assert lib().oracle_undistort_keypoints(_p(kps), len(kps), _p(k), _p(d), _p(out)) == 0
+    return out
+
+
+def compute_image_bounds(cols, rows, K4, dist4):
+    b = _Bounds()
+    k, d = np.ascontiguousarray(K4, np.float32), np.ascontiguousarray(dist4, np.float32)
+    assert lib().oracle_compute_image_bounds(cols, rows, _p(k), _p(d), ctypes.byref(b)) == 0
+    return (b.min_x, b.max_x, b.min_y, b.max_y)
 
 
 # ---- the rest of the ORBmatcher family (oracle/orb_oracle_match.cpp) -----------------------
