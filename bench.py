@@ -694,7 +694,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3")
     ap.add_argument("--batch", type=int, default=512, help="frames per step per GPU (c3, c4)")
-    ap.add_argument("--frames-per-stream", type=int, default=128, help="frames of each stream per step (c5)")
+    # 512: at N = 8 every rank keeps one stream of 512 frames, the batch size at which the
+    # per-frame rate has saturated (1280x720: B = 128 / 256 / 512 / 1024 -> 69 / 82 / 95 / 96k
+    # frames/s on one GPU, profiles/r03_v2_c5_batch_sweep.txt)
+    ap.add_argument("--frames-per-stream", type=int, default=512, help="frames of each stream per step (c5)")
     ap.add_argument("--width", type=int, default=0, help="override the preset (0 = preset)")
     ap.add_argument("--height", type=int, default=0)
     ap.add_argument("--nfeatures", type=int, default=0)

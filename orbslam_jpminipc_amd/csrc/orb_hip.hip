@@ -839,6 +839,38 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
 #endif
 }
 
+typedef short i16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// Compass pre-filter of cv::FAST for the 4 pixels of a dword, in packed 16-bit arithmetic:
+// even and odd bytes are split into u16 pairs.  Bright: (q0 > v+t or q8 > v+t) and (q4 or q12
+// likewise) <=> min(max(q0, q8), max(q4, q12)) > v + t; dark: max(min(q0, q8), min(q4, q12))
+// < v - t; each comparison is the sign of an i16 difference (all values within i16).
+// Returns a 4-bit mask (bit j = pixel j passes).
+__device__ __forceinline__ uint32_t compass4(uint32_t c, uint32_t q0, uint32_t q4, uint32_t q8, uint32_t q12,
+                                             uint32_t tt) {
+    uint32_t pass[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const uint32_t sel = h ? 0x0c030c01u : 0x0c020c00u;  // odd / even bytes -> u16 lanes
+        const i16x2 v = __builtin_bit_cast(i16x2, __builtin_amdgcn_perm(0u, c, sel));
+        const u16x2 a = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(0u, q0, sel));
+        const u16x2 b = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(0u, q4, sel));
+        const u16x2 d = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(0u, q8, sel));
+        const u16x2 e = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(0u, q12, sel));
+        const i16x2 t = __builtin_bit_cast(i16x2, tt);
+        const i16x2 M = __builtin_bit_cast(
+            i16x2, __builtin_elementwise_min(__builtin_elementwise_max(a, d), __builtin_elementwise_max(b, e)));
+        const i16x2 m = __builtin_bit_cast(
+            i16x2, __builtin_elementwise_max(__builtin_elementwise_min(a, d), __builtin_elementwise_min(b, e)));
+        const uint32_t br = __builtin_bit_cast(uint32_t, (i16x2)((v + t) - M));  // < 0: bright
+        const uint32_t dk = __builtin_bit_cast(uint32_t, (i16x2)(m - (v - t)));  // < 0: dark
+        pass[h] = (br | dk) & 0x80008000u;
+    }
+    // bit 15 / 31 of even -> pixels 0 / 2, of odd -> pixels 1 / 3
+    return ((pass[0] >> 15) & 1u) | ((pass[1] >> 14) & 2u) | ((pass[0] >> 29) & 4u) | ((pass[1] >> 28) & 8u);
+}
+
 // ---- FAST strength --------------------------------------------------------------------------
 // S(p) = 1 + cornerScore<16>(p) of cv::FAST: the largest t for which p is a corner is S - 1,
 // so p is a corner at threshold t <=> S > t; records carry S - 1 as the score.
@@ -910,7 +942,7 @@ __device__ __forceinline__ int fast_strength_packed(const uint8_t* p, int TP) {
 // Mat), survivors written in raster order as ((S - 1) << 24) | (y << 12) | x.  Returns the
 // survivor count (all threads).  smem: Sp (dwp x dh) | Fl (dwp x dh) | rowc | In, rerun_lds()
 // bytes.
-#define RR_Q 128  // per-wave queue of compass survivors (< 64 carried + 64 new), + a trash slot
+#define RR_Q 320  // per-wave queue of compass survivors (< 64 carried + 4 x 64 new), + a trash slot
 inline size_t rerun_lds(int dw, int dh) {
     const size_t dwp = (size_t)((dw + 3) & ~3), inW = (size_t)((3 + dw + 6 + 3) & ~3);
     return 2 * dwp * dh + 4 * (size_t)((dh + 3) & ~3) + inW * (dh + 6) + 16 + 4 * (4 + 4 * (RR_Q + 8));
@@ -931,24 +963,34 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
         // all loads of a batch in flight before any LDS write (one round trip per 20 dwords
         // per thread, instead of one per row group)
         stage_rows_to_lds<256>((uint32_t*)In, nwr, src, pw, dh + 6, nwr, nwr, tid);
-        for (int i = tid; i < nw; i += 256) ((uint32_t*)Fl)[i] = 0u;
+        for (int i = tid; i < nw; i += 256) {
+            ((uint32_t*)Fl)[i] = 0u;
+            ((uint32_t*)Sp)[i] = 0u;  // a pixel the compass rejects keeps strength 0
+        }
     }
     __syncthreads();
     // the strength plane (corner at t <=> S > t; the NMS below reads only S > t, so a pixel
-    // known not to be a corner may hold 0): per wave, 64 pixels at a time through the compass
-    // test of cv::FAST at t (a 9-arc always covers two cyclically adjacent points of {0, 4, 8,
-    // 12}: a necessary condition), survivors queued, the exact strength computed in full
-    // 64-lane passes from the top of the queue (LDS accesses of one wave complete in order)
+    // known not to be a corner may hold 0): per wave, 64 staged dwords (4 pixels each) at a
+    // time through the compass test of cv::FAST at t in packed 16-bit arithmetic (compass4, as
+    // k_fast: a 9-arc always covers two cyclically adjacent points of {0, 4, 8, 12}, a
+    // necessary condition), survivors queued as pixel indices, the exact strength computed in
+    // full 64-lane passes from the top of the queue (LDS accesses of one wave complete in order)
     {
         uint32_t* q = (uint32_t*)(In + inW * (dh + 6)) + 4 + wave * (RR_Q + 8);  // after the staged ROI
-        const uint32_t m = (uint32_t)((0x100000000ull + dw - 1) / (uint64_t)dw);  // i / dw = umulhi(i, m)
+        // i / d = umulhi(i, ceil(2^32 / d)) for d >= 2 (the reciprocal of 1 does not fit 32 bits)
+        const uint32_t m = (uint32_t)((0x100000000ull + dw - 1) / (uint64_t)dw);
         const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-        const int total = dh * dw;
+        // staged dword columns holding detection pixels: In byte c = xx + 3 + o, xx in [0, dw)
+        const int wd0 = (3 + o) >> 2, nd = ((dw + 2 + o) >> 2) - wd0 + 1;
+        const uint32_t md = (uint32_t)((0x100000000ull + nd - 1) / (uint64_t)nd);
+        const int total = dh * nd, iw = inW >> 2;
+        const uint32_t tt = (uint32_t)t | ((uint32_t)t << 16);
+        const uint32_t* In32 = (const uint32_t*)In;
         int np = 0;
         auto pass = [&](int base, int n) {  // q[base .. base + n), n <= 64
             if (lane < n) {
                 const int i = q[base + lane];
-                const int yy = (int)__umulhi((uint32_t)i, m), xx = i - yy * dw;
+                const int yy = dw > 1 ? (int)__umulhi((uint32_t)i, m) : i, xx = i - yy * dw;
                 Sp[yy * dwp + xx] = (uint8_t)max(fast_strength_packed(In + (yy + 3) * inW + xx + 3 + o, inW), 0);
             }
         };
@@ -957,17 +999,26 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
             const bool last = i0 >= total;  // wave-uniform
             if (!last) {
                 const int i = i0 + lane;
-                bool c = false;
+                uint32_t mask = 0u;
+                int px0 = 0;
                 if (i < total) {
-                    const int yy = (int)__umulhi((uint32_t)i, m), xx = i - yy * dw;
-                    const uint8_t* p = In + (yy + 3) * inW + xx + 3 + o;
-                    const int v = p[0], q0 = p[3 * inW], q4 = p[3], q8 = p[-3 * inW], q12 = p[-3];
-                    c = min(max(q0, q8), max(q4, q12)) > v + t || max(min(q0, q8), min(q4, q12)) < v - t;
-                    Sp[yy * dwp + xx] = 0;
+                    const int yy = nd > 1 ? (int)__umulhi((uint32_t)i, md) : i, wd = wd0 + i - yy * nd;
+                    const uint32_t* row = In32 + (yy + 3) * iw + wd;
+                    const uint32_t cc = row[0], lf = row[-1], rg = row[1], up = row[-3 * iw], dn = row[3 * iw];
+                    const int xx0 = 4 * wd - 3 - o;  // detection column of byte 0
+                    const int lo = max(0, -xx0), hi = min(4, dw - xx0);
+                    const uint32_t cols = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+                    mask = compass4(cc, dn, __builtin_amdgcn_alignbyte(rg, cc, 3), up,
+                                    __builtin_amdgcn_alignbyte(cc, lf, 1), tt) & cols;
+                    px0 = yy * dw + xx0;
                 }
-                const uint64_t bm = __ballot(c);
-                q[c ? np + __popcll(bm & below) : RR_Q] = (uint32_t)i;  // RR_Q: trash slot
-                np += __popcll(bm);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const bool c = (mask >> j) & 1u;
+                    const uint64_t bm = __ballot(c);
+                    q[c ? np + __popcll(bm & below) : RR_Q] = (uint32_t)(px0 + j);  // RR_Q: trash slot
+                    np += __popcll(bm);
+                }
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             while (np >= 64 || (last && np > 0)) {
@@ -1539,38 +1590,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
 struct FastTile {
     int level, x0, y0;  // detection origin in level coordinates: x0 = 16 + 256 k, y0 = 16 + FT_H m
 };
-
-typedef short i16x2 __attribute__((ext_vector_type(2)));
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-
-// Compass pre-filter of cv::FAST for the 4 pixels of a dword, in packed 16-bit arithmetic:
-// even and odd bytes are split into u16 pairs.  Bright: (q0 > v+t or q8 > v+t) and (q4 or q12
-// likewise) <=> min(max(q0, q8), max(q4, q12)) > v + t; dark: max(min(q0, q8), min(q4, q12))
-// < v - t; each comparison is the sign of an i16 difference (all values within i16).
-// Returns a 4-bit mask (bit j = pixel j passes).
-__device__ __forceinline__ uint32_t compass4(uint32_t c, uint32_t q0, uint32_t q4, uint32_t q8, uint32_t q12,
-                                             uint32_t tt) {
-    uint32_t pass[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const uint32_t sel = h ? 0x0c030c01u : 0x0c020c00u;  // odd / even bytes -> u16 lanes
-        const i16x2 v = __builtin_bit_cast(i16x2, __builtin_amdgcn_perm(0u, c, sel));
-        const u16x2 a = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(0u, q0, sel));
-        const u16x2 b = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(0u, q4, sel));
-        const u16x2 d = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(0u, q8, sel));
-        const u16x2 e = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(0u, q12, sel));
-        const i16x2 t = __builtin_bit_cast(i16x2, tt);
-        const i16x2 M = __builtin_bit_cast(
-            i16x2, __builtin_elementwise_min(__builtin_elementwise_max(a, d), __builtin_elementwise_max(b, e)));
-        const i16x2 m = __builtin_bit_cast(
-            i16x2, __builtin_elementwise_max(__builtin_elementwise_min(a, d), __builtin_elementwise_min(b, e)));
-        const uint32_t br = __builtin_bit_cast(uint32_t, (i16x2)((v + t) - M));  // < 0: bright
-        const uint32_t dk = __builtin_bit_cast(uint32_t, (i16x2)(m - (v - t)));  // < 0: dark
-        pass[h] = (br | dk) & 0x80008000u;
-    }
-    // bit 15 / 31 of even -> pixels 0 / 2, of odd -> pixels 1 / 3
-    return ((pass[0] >> 15) & 1u) | ((pass[1] >> 14) & 2u) | ((pass[0] >> 29) & 4u) | ((pass[1] >> 28) & 8u);
-}
 
 #ifndef KF_WAVES
 #define KF_WAVES 0  // > 0: waves per SIMD the register allocation targets
