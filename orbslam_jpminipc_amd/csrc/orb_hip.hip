@@ -1561,34 +1561,40 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
 // over each level's detection region [16, detX1) x [16, detY1) (the union of the cells'
 // areas) finds every cell's corners; the NMS then applies each cell's own boundary.
 //
-// k_fast: one 256-thread workgroup per FT_W x FT_H detection tile of a level, per frame.
-//   (1) stage the tile with its halo (rows y0-4 .. y0+FT_H+3, columns x0-16 .. x0+271) into
-//       LDS with 16-byte loads, all in flight before any LDS write;
-//   (2) per wave, FT_RW rows: compass pre-filter of cv::FAST (a 9-arc always covers two
-//       cyclically adjacent points of {0, 4, 8, 12}) on the lane's 4 pixels, packed 16-bit;
-//       lane-rows with a survivor are queued per wave;
-//   (3) the queue: full 9-arc test at fastTh with one pixel per lane (every lane busy), then
-//       the exact strength S (score = S - 1) of the corners, into an LDS strength plane that
-//       also holds the tile's 1-px halo ring (queued without pre-filter);
-//   (4) after one barrier, the per-cell 3x3 strict NMS from the plane; survivors are appended
-//       to their cell's candidate slots as ((S-1) << 24) | (y << 12) | x (k_select restores
-//       raster order).
+// k_fast: one 256-thread workgroup per detection tile of a level, per frame.  A tile is tw4
+// dwords (TW = 4 tw4 <= 256 columns, x0 a multiple of 4) by th rows: the level's detection width
+// is split evenly into ceil(width / 256) tiles, so few lanes fall outside the region, and th is
+// sized so the staged tile and the strength plane fit their LDS budgets.  The tile with its 1-px
+// strength ring is one flattened (plane row, dword) index space of (th + 2) x (tw4 + 2) dwords
+// (ring rows -1 and th; ring dwords -1 and tw4 contribute their one adjacent pixel), dealt to
+// the 4 waves 64 dwords at a time:
+//   (1) stage rows y0-4 .. y0+th+3, columns from the 16-aligned column at or below x0-8 to
+//       x0+TW+7, into LDS with 16-byte loads, all in flight before any LDS write;
+//   (2) compass pre-filter of cv::FAST (a 9-arc always covers two cyclically adjacent points of
+//       {0, 4, 8, 12}) on the lane's 4 pixels, packed 16-bit; dwords with a survivor inside the
+//       level's detection region are queued per wave;
+//   (3) the queue: expanded to one pixel per slot, the exact strength S (score = S - 1) in full
+//       64-pixel passes, `S > fastTh ? S : 0` into an LDS strength plane (a pixel the compass
+//       rejects is no corner at fastTh and keeps 0: the NMS only reads S > fastTh);
+//   (4) after one barrier, the plane's interior corners (flattened again) and the per-cell 3x3
+//       strict NMS; survivors are appended to their cell's candidate slots as
+//       ((S-1) << 24) | (y << 12) | x (k_select restores raster order).
 // The 7x7 blur of the descriptors is not materialised: k_orient_desc evaluates it at the
 // rBRIEF sample points from a raw window (ORBextractor.cc:760).
-#define FT_W 256  // detection columns per tile: 64 lanes x 4 pixels
-#ifndef FT_RW
-#define FT_RW 9   // detection rows per wave
-#endif
-#define FT_H (4 * FT_RW)      // detection rows per tile
-#define FT_IN_P 288           // staged row pitch (bytes): level columns x0-16 .. x0+271 (18 x 16 B)
-#define FT_IN_R (FT_H + 8)    // staged rows y0-4 .. y0+FT_H+3
-#define FT_SPW 264            // strength-plane row pitch (bytes): tile columns -4 .. 259
+#define FT_TW_MAX 256     // detection columns per tile at most (64 lanes x 4 pixels)
+#define FT_IN_BYTES 12672  // staged-tile LDS budget (44 rows of 288 B at TW = 256)
+#define FT_S_BYTES 10032   // strength-plane LDS budget (38 rows of 264 B at TW = 256)
 #ifndef FT_Q
-#define FT_Q 512              // per-wave queue (u16 entries): lane-rows, then the NMS corner list
+#define FT_Q 512           // per-wave queue (u16 entries): dwords, then the NMS corner list
 #endif
-#define FT_CQ 320             // per-wave pixel list (u16 entries): < 64 carried + 256 expanded
+#define FT_CQ 320          // per-wave pixel list (u16 entries): < 64 carried + 256 expanded
 struct FastTile {
-    int level, x0, y0;  // detection origin in level coordinates: x0 = 16 + 256 k, y0 = 16 + FT_H m
+    int level, x0, y0;  // detection origin (level coordinates); x0 = 16 + k TW, a multiple of 4
+    int tw4, th;        // dwords per row (>= 2), rows (clipped to the detection region)
+    int sp, sx;         // staged row pitch (bytes, a multiple of 16); x0 - first staged column (8 .. 23)
+    uint32_t rcpF;      // ceil(2^32 / (tw4 + 2)): flattened ring index -> plane row
+    uint32_t rcpI;      // ceil(2^32 / tw4): interior index -> row
+    uint32_t rcpU;      // ceil(2^32 / (sp / 16)): staged unit -> row
 };
 
 #ifndef KF_WAVES
@@ -1602,47 +1608,54 @@ struct FastTile {
 __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict__ pyr, Geom g,
                                                       const FastTile* __restrict__ tiles,
                                                       uint32_t* __restrict__ cand, int* __restrict__ cellCount) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_in[FT_IN_R * FT_IN_P];
-    __shared__ __attribute__((aligned(16))) uint8_t s_S[(FT_H + 2) * FT_SPW];
+    __shared__ __attribute__((aligned(16))) uint8_t s_in[FT_IN_BYTES];
+    __shared__ __attribute__((aligned(16))) uint8_t s_S[FT_S_BYTES];
     // per-wave lists; the last slot of each is a trash slot, so ballot-compacted appends store
     // unconditionally (no exec-mask branch per append)
     __shared__ uint16_t s_q[4][FT_Q + 2];
     __shared__ uint16_t s_px[4][FT_CQ + 2];  // a chunk's pixels, compacted in place to its corners
     KF_T(0);
-    const FastTile t = tiles[blockIdx.x];
+    FastTile t = tiles[blockIdx.x];
     const int b = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    // the level's geometry in SGPRs for the whole kernel (read through a reference into the
-    // kernarg block, the compiler re-issued dependent s_loads inside the loops); the empty asm
-    // makes the copies opaque, so they cannot be rematerialised
+    // the level's geometry and the tile in SGPRs for the whole kernel (read through a reference
+    // into the kernarg block, the compiler re-issued dependent s_loads inside the loops); the
+    // empty asm makes the copies opaque, so they cannot be rematerialised
     LevelGeom lg = g.lv[t.level];
     asm volatile("" : "+s"(lg.w), "+s"(lg.h), "+s"(lg.pitch), "+s"(lg.ph), "+s"(lg.detX1), "+s"(lg.detY1),
                  "+s"(lg.rows), "+s"(lg.cols));
     asm volatile("" : "+s"(lg.cellW), "+s"(lg.cellH), "+s"(lg.cellWm), "+s"(lg.cellHm), "+s"(lg.cell0),
                  "+s"(lg.base), "+s"(lg.fstride), "+s"(lg.candBase), "+s"(lg.capMax));
-    {  // (1) stage: padded rows y0+12 .. (clipped to the buffer), padded columns x0 .. x0+287
-        // (16-byte aligned: x0 = 16 + 256 k and the pitch is a multiple of 16), clipped to the row
+    asm volatile("" : "+s"(t.x0), "+s"(t.y0), "+s"(t.tw4), "+s"(t.th), "+s"(t.sp), "+s"(t.sx), "+s"(t.rcpF),
+                 "+s"(t.rcpI));
+    const int fw = t.tw4 + 2;          // flattened row width (dwords): ring dword -1 .. tw4
+    const int spw = 4 * t.tw4 + 8;     // strength-plane pitch: tile columns -4 .. TW+3
+    {  // (1) stage: padded rows y0+12 .. (clipped to the buffer), t.sp bytes from the 16-aligned
+       // padded column x0+16-sx (clipped to the row)
         const uint8_t* src = pyr + lg.base + (long long)b * lg.fstride;
-        const int pr0 = t.y0 - 4 + EDGE;
-        const int rows = min(FT_IN_R, lg.ph - pr0);
-        const int units = min(FT_IN_P / 16, (lg.pitch - t.x0) >> 4);
-        const uint4* gs = (const uint4*)(src + (long long)pr0 * lg.pitch + t.x0);
+        const int pr0 = t.y0 - 4 + EDGE, pc0 = t.x0 - t.sx + EDGE;
+        const int upr = t.sp >> 4;
+        const int rows = min(t.th + 8, lg.ph - pr0);
+        const int units = min(upr, (lg.pitch - pc0) >> 4);
+        const int nU = (t.th + 8) * upr;  // <= FT_IN_BYTES / 16
+        const uint4* gs = (const uint4*)(src + (long long)pr0 * lg.pitch + pc0);
         const int gsu = lg.pitch >> 4;
-        constexpr int NU = (FT_IN_R * (FT_IN_P / 16) + 255) / 256;
+        constexpr int NU = (FT_IN_BYTES / 16 + 255) / 256;
         uint4 v[NU];
 #pragma unroll
         for (int k = 0; k < NU; ++k) {
             const int i = tid + 256 * k;
-            const int r = i / (FT_IN_P / 16), u = i - r * (FT_IN_P / 16);
-            const bool ok = r < rows && u < units;
+            const int r = (int)__umulhi((uint32_t)i, t.rcpU), u = i - r * upr;
+            const bool ok = i < nU && r < rows && u < units;
             v[k] = gs[ok ? (long long)r * gsu + u : 0ll];  // every slot loads (no scratch spill)
             if (!ok) v[k] = make_uint4(0u, 0u, 0u, 0u);
         }
 #pragma unroll
         for (int k = 0; k < NU; ++k) {
             const int i = tid + 256 * k;
-            if (i < FT_IN_R * (FT_IN_P / 16)) ((uint4*)s_in)[i] = v[k];
+            if (i < nU) ((uint4*)s_in)[i] = v[k];
         }
-        for (int i = tid; i < (FT_H + 2) * FT_SPW / 16; i += 256) ((uint4*)s_S)[i] = make_uint4(0u, 0u, 0u, 0u);
+        const int nS = ((t.th + 2) * spw) >> 2;
+        for (int i = tid; i < nS; i += 256) ((uint32_t*)s_S)[i] = 0u;
     }
     __syncthreads();
     KF_T(1);
@@ -1651,37 +1664,31 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
     const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint16_t* pq = s_q[wave];
     uint16_t* px = s_px[wave];
-    const uint8_t* inb = s_in;
-    const int x = t.x0 + 4 * lane;  // first of this lane's 4 columns
-    const int rBase = wave * FT_RW - 1;  // tile row of rowCode 0
-    uint32_t colMask = 0;  // detection-region columns of this lane (x >= 16 always)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) colMask |= (uint32_t)(x + j < lg.detX1) << j;
-    // (3) the queue: full 9-arc test + exact strength of pq[0 .. qn), all lanes busy; corners
-    // -> strength plane.  u16 entry = rowCode << 11 | laneCode << 4 | mask: tile row
-    // rBase + rowCode, bit j of mask is tile column 4 * (laneCode - 1) + j (laneCode 0 and 65
-    // carry the halo columns -1 and 256).  Pixel code = (tile row + 1) << 9 | (tile col + 1).
-    // pixels expanded from the queue wait in px until a full pass of 64 is ready (partial
-    // passes only at the very end), so the strength passes run with every lane busy
+    // pixel code = plane row << 9 | plane column (plane row = tile row + 1, plane column = tile
+    // column + 1); staged byte of a pixel: row pr + 3, column sx + pc - 1
     int np = 0;
     auto strength_pass = [&](int base, int n) {  // px[base .. base + n), n <= 64
         if (lane < n) {
             const uint16_t c = px[base + lane];
-            const int S = fast_strength_packed(inb + ((c >> 9) + 3) * FT_IN_P + (c & 511) + 15, FT_IN_P);
-            s_S[(c >> 9) * FT_SPW + (c & 511) + 3] = (uint8_t)(S > ft ? S : 0);  // each pixel once
+            const int S = fast_strength_packed(s_in + ((c >> 9) + 3) * t.sp + t.sx + (c & 511) - 1, t.sp);
+            s_S[(c >> 9) * spw + (c & 511) + 3] = (uint8_t)(S > ft ? S : 0);  // each pixel once
         }
     };
+    // queue entry = flattened index f << 4 | mask (bit j: pixel j of dword f); f = pr * fw + dc,
+    // dword dc - 1 of plane row pr, pixel j at plane column 4 dc + j - 3
     auto drain = [&](int qn) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         for (int i0 = 0; i0 < qn; i0 += 64) {
             const int i = i0 + lane;
             const uint32_t e = i < qn ? pq[i] : 0u;
-            const int rt = rBase + (int)(e >> 11), cb = 4 * ((int)((e >> 4) & 127) - 1);
+            const int f = (int)(e >> 4);
+            const int pr = (int)__umulhi((uint32_t)f, t.rcpF), dc = f - pr * fw;
+            const uint32_t code = ((uint32_t)pr << 9) + 4u * (uint32_t)dc - 3u;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {  // expand the 64 lane-row entries into one pixel per slot
+            for (int j = 0; j < 4; ++j) {  // expand the 64 entries into one pixel per slot
                 const bool v = (e >> j) & 1u;
                 const uint64_t m = __ballot(v);
-                px[v ? np + __popcll(m & below) : FT_CQ] = (uint16_t)(((rt + 1) << 9) | (cb + j + 1));
+                px[v ? np + __popcll(m & below) : FT_CQ] = (uint16_t)(code + j);
                 np += __popcll(m);
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1694,47 +1701,39 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     };
-    int qn = 0;
-    auto push = [&](uint32_t mask, int rt, int laneCode) {  // wave-uniform call
-        const bool v = mask != 0u;
-        const uint64_t m = __ballot(v);
-        pq[v ? qn + __popcll(m & below) : FT_Q] = (uint16_t)(((rt - rBase) << 11) | (laneCode << 4) | mask);
-        qn += __popcll(m);
-    };
-    {  // halo ring of the strength plane: rows -1 (wave 0) and FT_H (wave 3) over the tile's
-       // columns, columns -1 and 256 over rows -1 .. FT_H (no pre-filter)
-        if (wave == 0 || wave == 3) {
-            const int rt = wave == 0 ? -1 : FT_H;
-            const int Y = t.y0 + rt;
-            push((Y >= EDGE && Y < lg.detY1) ? colMask : 0u, rt, lane + 1);
+    // (2) compass pre-filter over the flattened tile + ring, 64 dwords per wave and step
+    {
+        int qn = 0;
+        const int nF = (t.th + 2) * fw, iw = t.sp >> 2;
+        for (int it = wave; it * 64 < nF; it += 4) {  // wave-uniform
+            const int f = it * 64 + lane;
+            uint32_t mask = 0u;
+            if (f < nF) {
+                const int pr = (int)__umulhi((uint32_t)f, t.rcpF), dc = f - pr * fw;
+                const int Y = t.y0 + pr - 1, X = t.x0 + 4 * (dc - 1);  // level row, column of byte 0
+                // ring dwords contribute their one pixel adjacent to the tile; every pixel must
+                // lie in the level's detection region [16, detX1) x [16, detY1)
+                const int lo = max(dc == 0 ? 3 : 0, EDGE - X), hi = min(dc == fw - 1 ? 1 : 4, lg.detX1 - X);
+                const uint32_t* row = (const uint32_t*)(s_in + (pr + 3) * t.sp + t.sx) + (dc - 1);
+                const uint32_t cc = row[0], lf = row[-1], rg = row[1], up = row[-3 * iw], dn = row[3 * iw];
+                if (Y >= EDGE && Y < lg.detY1 && lo < hi)
+                    mask = compass4(cc, dn, __builtin_amdgcn_alignbyte(rg, cc, 3), up,
+                                    __builtin_amdgcn_alignbyte(cc, lf, 1), tt) &
+                           (((1u << hi) - 1u) & ~((1u << lo) - 1u));
+            }
+            if (qn > FT_Q - 64) {
+                drain(qn);
+                qn = 0;
+            }
+            const bool v = mask != 0u;
+            const uint64_t m = __ballot(v);
+            pq[v ? qn + __popcll(m & below) : FT_Q] = (uint16_t)(((uint32_t)f << 4) | mask);
+            qn += __popcll(m);
         }
-        const int nr = FT_RW + (wave == 0) + (wave == 3);  // rows of this wave's column halo
-        const int r0 = wave * FT_RW - (wave == 0);
-        const int rt = r0 + (lane >> 1), right = lane & 1;
-        const int X = t.x0 + (right ? FT_W : -1), Y = t.y0 + rt;
-        const bool in = lane < 2 * nr && X >= EDGE && X < lg.detX1 && Y >= EDGE && Y < lg.detY1;
-        push(in ? (right ? 1u : 8u) : 0u, rt, right ? 65 : 0);
+        KF_T(2);
+        drain(qn);
+        if (np) strength_pass(0, np);  // the remainder, < 64 pixels
     }
-    // (2) compass pre-filter, row by row (wave-uniform rows)
-    const uint32_t* in32 = (const uint32_t*)s_in + 4 + lane;  // the lane's centre dword of staged row 0
-    for (int i = 0; i < FT_RW; ++i) {
-        const int rt = wave * FT_RW + i;
-        if (t.y0 + rt >= lg.detY1) break;
-        const uint32_t* row = in32 + (rt + 4) * (FT_IN_P / 4);
-        const uint32_t cc = row[0], lf = row[-1], rg = row[1];
-        const uint32_t up = row[-3 * (FT_IN_P / 4)], dn = row[3 * (FT_IN_P / 4)];
-        const uint32_t a4 = __builtin_amdgcn_alignbyte(rg, cc, 3);   // x+3 .. x+6
-        const uint32_t a12 = __builtin_amdgcn_alignbyte(cc, lf, 1);  // x-3 .. x
-        const uint32_t mask = compass4(cc, dn, a4, up, a12, tt) & colMask;
-        if (qn > FT_Q - 64) {
-            drain(qn);
-            qn = 0;
-        }
-        push(mask, rt, lane + 1);
-    }
-    KF_T(2);
-    drain(qn);
-    if (np) strength_pass(0, np);  // the remainder, < 64 pixels
     KF_T(3);
     __syncthreads();
     KF_T(4);
@@ -1743,7 +1742,6 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
     // ((y-16) / cellH, (x-16) / cellW) by exact reciprocal multiplies (host-checked).
     int* fcount = cellCount + (long long)b * g.nCells + lg.cell0;
     uint32_t* fcand = cand + (long long)b * g.candPerFrame + lg.candBase;
-    int cn = 0;
     auto nms_emit = [&](int n) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         int sn = 0;
@@ -1762,12 +1760,12 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
                     const int ylo = EDGE + ci * lg.cellH, yhi = ci == lg.rows - 1 ? lg.h - EDGE : ylo + lg.cellH;
                     // the plane holds the tile's 1-px ring, so all 9 reads are in bounds: issue
                     // them together (no per-neighbour branch), then mask the out-of-cell ones
-                    const uint8_t* sp = s_S + (rt + 1) * FT_SPW + ct + 4;
+                    const uint8_t* sp = s_S + (rt + 1) * spw + ct + 4;
                     int nbv[9];
 #pragma unroll
                     for (int dy = -1; dy <= 1; ++dy)
 #pragma unroll
-                        for (int dx = -1; dx <= 1; ++dx) nbv[(dy + 1) * 3 + dx + 1] = sp[dy * FT_SPW + dx];
+                        for (int dx = -1; dx <= 1; ++dx) nbv[(dy + 1) * 3 + dx + 1] = sp[dy * spw + dx];
                     const int S = nbv[4];
                     const bool xl = X - 1 >= xlo, xr = X + 1 < xhi, yu = Y - 1 >= ylo, yd = Y + 1 < yhi;
                     bool ok = true;
@@ -1795,32 +1793,42 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
             const int X = t.x0 + ct, Y = t.y0 + rt;
             const int c = (int)__umulhi((uint32_t)(Y - EDGE), (uint32_t)lg.cellHm) * lg.cols +
                           (int)__umulhi((uint32_t)(X - EDGE), (uint32_t)lg.cellWm);
-            const int S = s_S[(rt + 1) * FT_SPW + ct + 4];
+            const int S = s_S[(rt + 1) * spw + ct + 4];
             const int pos = atomicAdd(fcount + c, 1);
             if (pos < lg.capMax)
                 fcand[c * lg.capMax + pos] = ((uint32_t)(S - 1) << 24) | ((uint32_t)Y << 12) | (uint32_t)X;
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     };
-    // corners of the wave's rows (ballot-compacted from the plane), then the NMS on the list
-    for (int i = 0; i < FT_RW; ++i) {
-        const int rt = wave * FT_RW + i;
-        if (t.y0 + rt >= lg.detY1) break;  // wave-uniform
-        const uint32_t w4 = *(const uint32_t*)(s_S + (rt + 1) * FT_SPW + 4 + 4 * lane);
-        if (__ballot(w4 != 0u) == 0ull) continue;
+    // the plane's interior corners (ballot-compacted, flattened over th x tw4 dwords), then the
+    // NMS on the list
+    {
+        int cn = 0;
+        const int nI = t.th * t.tw4;
+        for (int it = wave; it * 64 < nI; it += 4) {  // wave-uniform
+            const int i = it * 64 + lane;
+            uint32_t w4 = 0u;
+            int r = 0, d = 0;
+            if (i < nI) {
+                r = (int)__umulhi((uint32_t)i, t.rcpI);
+                d = i - r * t.tw4;
+                w4 = *(const uint32_t*)(s_S + (r + 1) * spw + 4 + 4 * d);
+            }
+            if (__ballot(w4 != 0u) == 0ull) continue;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const bool v = ((w4 >> (8 * j)) & 0xFFu) != 0u;
-            const uint64_t m = __ballot(v);
-            pq[v ? cn + __popcll(m & below) : FT_Q] = (uint16_t)((rt << 9) | (4 * lane + j));
-            cn += __popcll(m);
+            for (int j = 0; j < 4; ++j) {
+                const bool v = ((w4 >> (8 * j)) & 0xFFu) != 0u;
+                const uint64_t m = __ballot(v);
+                pq[v ? cn + __popcll(m & below) : FT_Q] = (uint16_t)((r << 9) | (4 * d + j));
+                cn += __popcll(m);
+            }
+            if (cn > FT_Q - 256) {
+                nms_emit(cn);
+                cn = 0;
+            }
         }
-        if (cn > FT_Q - 256) {
-            nms_emit(cn);
-            cn = 0;
-        }
+        if (cn) nms_emit(cn);
     }
-    if (cn) nms_emit(cn);
 #if KF_TIMING
     KF_T(5);
     if (lane == 0) {
@@ -2993,10 +3001,26 @@ struct orb_extractor {
         // workspace
         // + slack: k_orient_desc's 64-byte window rows may over-read the last row's pitch
         HIP_TRY(hipMalloc(&d_pyr, (size_t)pyrBytes + 256));
-        std::vector<FastTile> tl;  // k_fast tiles over each level's detection region
-        for (int l = 0; l < nlevels; ++l)
-            for (int y0 = orbdev::EDGE; y0 < G.lv[l].detY1; y0 += FT_H)
-                for (int x0 = orbdev::EDGE; x0 < G.lv[l].detX1; x0 += FT_W) tl.push_back(FastTile{l, x0, y0});
+        // k_fast tiles over each level's detection region: the width split evenly into
+        // ceil(width / 256) tiles of a multiple of 4 columns, as many rows as the LDS budgets
+        // (staged tile, strength plane) and the 16-bit queue codes allow
+        std::vector<FastTile> tl;
+        auto rcp = [](int d) { return (uint32_t)((0x100000000ull + (uint64_t)d - 1) / (uint64_t)d); };
+        for (int l = 0; l < nlevels; ++l) {
+            const int detW = G.lv[l].detX1 - orbdev::EDGE;
+            const int nx = (detW + FT_TW_MAX - 1) / FT_TW_MAX;
+            const int tw4 = std::max(2, ((detW + 3) / 4 + nx - 1) / nx), TW = 4 * tw4;
+            for (int x0 = orbdev::EDGE; x0 < G.lv[l].detX1; x0 += TW) {
+                const int sx = x0 - (((x0 + orbdev::EDGE - 8) & ~15) - orbdev::EDGE);
+                const int sp = (sx + TW + 8 + 15) & ~15, spw = TW + 8;
+                const int thMax = std::min({FT_IN_BYTES / sp - 8, FT_S_BYTES / spw - 2, 126, 4095 / (tw4 + 2) - 2});
+                if (thMax < 1 || sp > 288) return set_err(ORB_EINVAL, "k_fast tile geometry");
+                for (int y0 = orbdev::EDGE; y0 < G.lv[l].detY1; y0 += thMax) {
+                    const int th = std::min(thMax, G.lv[l].detY1 - y0);
+                    tl.push_back(FastTile{l, x0, y0, tw4, th, sp, sx, rcp(tw4 + 2), rcp(tw4), rcp(sp >> 4)});
+                }
+            }
+        }
         HIP_TRY(hipMalloc(&d_tiles, tl.size() * sizeof(FastTile)));
         HIP_TRY(hipMemcpy(d_tiles, tl.data(), tl.size() * sizeof(FastTile), hipMemcpyHostToDevice));
         nTiles = (int)tl.size();
