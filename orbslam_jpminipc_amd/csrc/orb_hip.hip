@@ -1581,9 +1581,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
 //       ((S-1) << 24) | (y << 12) | x (k_select restores raster order).
 // The 7x7 blur of the descriptors is not materialised: k_orient_desc evaluates it at the
 // rBRIEF sample points from a raw window (ORBextractor.cc:760).
+#ifndef FT_TW_MAX
 #define FT_TW_MAX 256     // detection columns per tile at most (64 lanes x 4 pixels)
+#endif
+#ifndef FT_IN_BYTES
 #define FT_IN_BYTES 12672  // staged-tile LDS budget (44 rows of 288 B at TW = 256)
+#endif
+#ifndef FT_S_BYTES
 #define FT_S_BYTES 10032   // strength-plane LDS budget (38 rows of 264 B at TW = 256)
+#endif
 #ifndef FT_Q
 #define FT_Q 512           // per-wave queue (u16 entries): dwords, then the NMS corner list
 #endif
