@@ -139,4 +139,23 @@ __device__ __forceinline__ int fast_strength(int v, const int* c, int tmin) {
     return max(A, Bn);
 }
 
+// ---- wave64 cross-lane arithmetic on DPP (VALU only) ---------------------------------------
+// __shfl_up / __shfl_xor compile to ds_bpermute_b32: every step is an LDS round trip.  DPP
+// moves data between lanes inside the VALU instruction: row_shr:n within each 16-lane row,
+// row_bcast:15 / row_bcast:31 across rows (GFX9 DPP16).
+// Inclusive prefix sum over the 64 lanes.
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+    return v;
+}
+// Sum over the 64 lanes, wave-uniform.
+__device__ __forceinline__ int wave_total(int v) { return __builtin_amdgcn_readlane(wave_incl_scan(v), 63); }
+// The value of lane ^ 1.
+__device__ __forceinline__ int lane_xor1(int v) { return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, false); }
+
 }  // namespace orbdev

@@ -1065,14 +1065,9 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
         for (int r0 = 0; r0 < dh; r0 += 64) {
             const int r = r0 + lane;
             const int v = r < dh ? rowc[r] : 0;
-            int incl = v;
-#pragma unroll
-            for (int o2 = 1; o2 < 64; o2 <<= 1) {
-                const int nb = __shfl_up(incl, o2, 64);
-                if (lane >= o2) incl += nb;
-            }
+            const int incl = wave_incl_scan(v);
             if (r < dh) rowc[r] = carry + incl - v;
-            carry += __shfl(incl, 63, 64);
+            carry += __builtin_amdgcn_readlane(incl, 63);
         }
         if (lane == 0) s_total = carry;
     }
@@ -1084,12 +1079,7 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
             const int w = w0 + lane;
             const uint32_t f = w < rw ? Flw[yy * rw + w] : 0u;
             const int n = __popc(f);
-            int incl = n;
-#pragma unroll
-            for (int o2 = 1; o2 < 64; o2 <<= 1) {
-                const int nb = __shfl_up(incl, o2, 64);
-                if (lane >= o2) incl += nb;
-            }
+            const int incl = wave_incl_scan(n);
             int pos = off + incl - n;
 #pragma unroll
             for (int j2 = 0; j2 < 4; ++j2)
@@ -1098,7 +1088,7 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
                     const uint32_t sc = (uint32_t)(Sp[yy * dwp + xx] - 1);
                     out[pos++] = (sc << 24) | ly | (uint32_t)(rx0 + xx);
                 }
-            off += __shfl(incl, 63, 64);
+            off += __builtin_amdgcn_readlane(incl, 63);
         }
     }
     const int total = s_total;
@@ -1227,23 +1217,14 @@ __device__ __forceinline__ void wave_prefix(int* dst, const int* src, int n, int
     for (int c0 = 0; c0 < n; c0 += 64) {
         const int c = c0 + lane;
         const int v = c < n ? src[c] : 0;
-        int incl = v;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int nb = __shfl_up(incl, o, 64);
-            if (lane >= o) incl += nb;
-        }
+        const int incl = wave_incl_scan(v);
         if (c < n) dst[c] = carry + incl - v;
-        carry += __shfl(incl, 63, 64);
+        carry += __builtin_amdgcn_readlane(incl, 63);
     }
     if (lane == 0) dst[n] = carry;
 }
 
-__device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
+__device__ __forceinline__ int wave_sum(int v) { return wave_total(v); }
 
 // Cell of list element i: the last c in [0, n) with off[c] <= i (off ascending, off[0] = 0).
 __device__ __forceinline__ int cell_of(const int* off, int n, int i) {
@@ -2053,11 +2034,8 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
             }
         }
     }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-        m01 += __shfl_xor(m01, o, 64);
-        m10 += __shfl_xor(m10, o, 64);
-    }
+    m01 = wave_total(m01);
+    m10 = wave_total(m10);
     const float angle = fast_atan2((float)m01, (float)m10);
     // computeOrbDescriptor (ORBextractor.cc:155-194)
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
@@ -2095,7 +2073,7 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
     int nib = 0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) nib |= (vals[2 * q] < vals[2 * q + 1]) << q;
-    const int other = __shfl_xor(nib, 1, 64);
+    const int other = lane_xor1(nib);
     const long long kslot = (long long)b * g.kpCap + before + idx;
     if ((lane & 1) == 0) desc[kslot * 32 + (lane >> 1)] = (uint8_t)(nib | (other << 4));
     if (lane == 0) {
@@ -2548,8 +2526,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
             }
         }
     }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) nm += __shfl_xor(nm, o, 64);
+    nm = wave_total(nm);
     if (lane == 0) s_hist[wave] = nm;
     __syncthreads();
     if (tid == 0) A.nmOut[p] = s_hist[0] + s_hist[1] + s_hist[2] + s_hist[3];

@@ -1,0 +1,37 @@
+#!/usr/bin/env python3
+"""Build a timing-ablation variant of liborb_hip.so from a patched copy of the sources (the
+product sources are never modified): ablation_variant.py NAME 'old1' 'new1' ['old2' 'new2' ...]
+applies exact-string replacements to orb_hip.hip in a scratch copy and builds
+build/variants/NAME.so.  Wrong-output ablations live only in these scratch builds."""
+import pathlib
+import shutil
+import subprocess
+import sys
+import tempfile
+
+ROOT = pathlib.Path(__file__).resolve().parent.parent
+name, reps = sys.argv[1], sys.argv[2:]
+tmp = pathlib.Path(tempfile.mkdtemp(prefix="orbvar_"))
+shutil.copytree(ROOT / "orbslam_jpminipc_amd" / "csrc", tmp / "csrc")
+shutil.copytree(ROOT / "include", tmp / "include")
+src = tmp / "csrc" / "orb_hip.hip"
+s = src.read_text()
+for a, b in zip(reps[0::2], reps[1::2]):
+    if s.count(a) != 1:
+        sys.exit(f"pattern occurs {s.count(a)} times: {a[:80]!r}")
+    s = s.replace(a, b)
+src.write_text(s.replace('#include "../../include/orb_abi.h"', '#include "../include/orb_abi.h"'))
+for f in (tmp / "csrc").glob("*.hip"):
+    t = f.read_text().replace('"../../include/orb_abi.h"', '"../include/orb_abi.h"')
+    f.write_text(t)
+units = [tmp / "csrc" / u for u in ("orb_hip.hip", "orb_match.hip", "orb_voc.hip", "orb_mappoint.hip",
+                                    "orb_pipeline.hip", "orb_persist.hip", "orb_frame.hip")]
+out = ROOT / "build" / "variants" / f"{name}.so"
+out.parent.mkdir(parents=True, exist_ok=True)
+flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
+         "-fno-gpu-flush-denormals-to-zero", "-fhip-fp32-correctly-rounded-divide-sqrt"]
+r = subprocess.run(["/opt/rocm/bin/hipcc", *flags, "-o", str(out), *map(str, units)], capture_output=True, text=True)
+shutil.rmtree(tmp)
+if r.returncode:
+    sys.exit(r.stderr[-3000:])
+print("built", out)
