@@ -25,6 +25,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/orb_abi.h"
@@ -131,7 +132,9 @@ __constant__ float c_patternf[1024];  // the same pattern as floats: lane l's 8 
 // IC_Angle disc masks (ORBextractor.cc:124-151 with umax, 495-510) of the 31 x 9 patch dwords for
 // each byte alignment sh of the patch in its dword row: byte i of dword n = 9 r + c is inside the
 // disc iff |4c + i - sh - 15| <= umax[|r - 15|]
-__constant__ uint32_t c_icmask[4 * 320];  // 279 patch dwords per alignment, zero-padded to 5 x 64
+__constant__ uint32_t c_icmask[4 * 320];
+// k_orient_desc's row-pass B fragments: [N-tile t][lane l] = bytes j of B[16(l >> 4) + j][16t + (l & 15)]
+__constant__ uint4 c_rowB[4 * 64];  // 279 patch dwords per alignment, zero-padded to 5 x 64
 // ---- pyramid --------------------------------------------------------------------------
 // Level 0: copyMakeBorder(image, 16, BORDER_REFLECT_101); one thread per 16-byte chunk of a
 // padded row (pitch is a multiple of 16).  Interior chunks (source columns [x-16, x) inside the
@@ -1855,11 +1858,12 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
 #endif
 #define OD_HC 40   // row-pass columns: x-18 .. x+21 (10 groups of 4)
 #define OD_HPR 22  // row pairs of the row-pass sums (window rows 0 .. 43)
-// byte offset of the sums in the wave's buffer: the first row-pass round's writes (from byte
-// OD_HOFF + 160 * 8) must stay above window row 20, the last one the second round reads
-#define OD_HOFF (OD_WP == 64 ? 128 : 21 * OD_WP - 8 * 160)
-#define GT_WA 0x37312212u  // bytes (x-3, x-2, x-1, x) -> 18, 34, 49, 55
-#define GT_WB 0x00122231u  // bytes (x+1, x+2, x+3, x+4) -> 49, 34, 18, 0
+#define OD_HN 56   // row-pass sum columns per pair row (window columns n = 0 .. 55 >= o0 + 39; hc = n - o0)
+#define OD_BUF (OD_HPR * OD_HN * 4)  // per-wave LDS: the 44-row window, then (overlaid) the sums
+static_assert(48 * OD_WP <= OD_BUF, "window rows 0 .. 47 inside the wave's buffer");
+typedef int i32x4v __attribute__((ext_vector_type(4)));
+// first window row of the three row-pass M-tiles (rows 28 .. 31 computed twice, identically)
+__device__ constexpr int kOdRow[3] = {0, 16, 28};
 // column-pass taps over row pairs (low half = the even row): rows r0-3 .. r0+4 when r0 is even
 #define GP_E0 (18u | (34u << 16))
 #define GP_E1 (49u | (55u << 16))
@@ -1876,29 +1880,24 @@ __device__ __forceinline__ uint32_t dot2u(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2v, a), __builtin_bit_cast(u16x2v, b), c, false);
 }
 
-// Row pass of the 7-tap kernel for 4 consecutive outputs whose 10 input bytes start at byte
-// 0 of (a, b, c) (bytes 0-3, 4-7, 8-11): output j reads bytes j .. j+6.
-__device__ __forceinline__ void hrow4(uint32_t a, uint32_t b, uint32_t c, uint32_t* h) {
-    h[0] = __builtin_amdgcn_udot4(a, GT_WA, __builtin_amdgcn_udot4(b, GT_WB, 0u, false), false);
-    h[1] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(b, a, 1), GT_WA,
-                                  __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(c, b, 1), GT_WB, 0u, false), false);
-    h[2] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(b, a, 2), GT_WA,
-                                  __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(c, b, 2), GT_WB, 0u, false), false);
-    h[3] = __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(b, a, 3), GT_WA,
-                                  __builtin_amdgcn_udot4(__builtin_amdgcn_alignbyte(c, b, 3), GT_WB, 0u, false), false);
-}
-
 // Column pass at window column hc (= dx + 18), sums of window rows r0 .. r0+6 (r0 = dy + 18):
 // T = sum_j k_j H(r0 + 3 + j).  Row pairs p0 .. p0+3 hold rows 2 p0 .. 2 p0 + 7; for odd r0 the
 // taps shift by one row (one u16 lane).
 __device__ __forceinline__ uint32_t vpass(const uint32_t* __restrict__ Hs, int r0, int hc) {
     const int p0 = r0 >> 1;
-    const uint32_t* q = Hs + p0 * OD_HC + hc;
-    const uint32_t h0 = q[0], h1 = q[OD_HC], h2 = q[2 * OD_HC], h3 = q[3 * OD_HC];
+    const uint32_t* q = Hs + p0 * OD_HN + hc;
+    const uint32_t h0 = q[0], h1 = q[OD_HN], h2 = q[2 * OD_HN], h3 = q[3 * OD_HN];
     const bool odd = r0 & 1;
     const uint32_t t0 = odd ? GP_O0 : GP_E0, t1 = odd ? GP_O1 : GP_E1;
     const uint32_t t2 = odd ? GP_O2 : GP_E2, t3 = odd ? GP_O3 : GP_E3;
     return dot2u(h3, t3, dot2u(h2, t2, dot2u(h1, t1, dot2u(h0, t0, 0u))));
+}
+
+// (m & a) | (~m & b) in one VALU
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+    return r;
 }
 
 // cvRound-equivalent of T / 65536: half to even (SSE2 columns) or half up (scalar tail), then
@@ -1913,8 +1912,8 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
                                                      const int* __restrict__ lvlCount, orb_keypoint_t* __restrict__ kps,
                                                      uint8_t* __restrict__ desc, int* __restrict__ counts,
                                                      const float* __restrict__ lvlResp) {
-    // per wave: the raw window, then (overlaid, OD_HOFF bytes in) the row-pass sums
-    __shared__ __attribute__((aligned(16))) uint8_t s_buf[4][OD_HOFF + OD_HPR * OD_HC * 4];
+    // per wave: the raw window, then (overlaid) the row-pass sums
+    __shared__ __attribute__((aligned(16))) uint8_t s_buf[4][OD_BUF];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     // XCD-aware block order: workgroup i runs on XCD i % 8, so give each XCD a contiguous run
     // of keypoints (neighbouring keypoints share window rows: L2 hits instead of HBM re-reads)
@@ -1949,7 +1948,10 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
                                       (long long)(y + EDGE - OD_WR) * lg.pitch + xa);
     const uint32_t pu = (uint32_t)lg.pitch >> 4;
     uint8_t* W = s_buf[wave];
-    uint32_t* Hs = (uint32_t*)(s_buf[wave] + OD_HOFF);
+    uint32_t* Hs = (uint32_t*)s_buf[wave];
+    i32x4v Bf[4];  // the row pass's B fragments (constant; in flight with the window loads)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) Bf[t] = __builtin_bit_cast(i32x4v, c_rowB[t * 64 + lane]);
     {
         constexpr int NU = (2 * OD_WR + 1) * 4;  // 172 16-byte units
         uint4 v[3];
@@ -1960,8 +1962,6 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
         }
         // all 192 units stored (units >= 172 repeat unit 0 into the buffer's unused tail,
         // before the row-pass sums are written): no masked store
-        static_assert(48 * OD_WP <= OD_HOFF + OD_HPR * OD_HC * 4, "window tail inside the wave's buffer");
-        static_assert(OD_HOFF + 8 * 160 >= 20 * OD_WP, "first-round sums above the second round's rows");
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
             const int i = lane + 64 * j;
@@ -1993,45 +1993,47 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
             m01 += __mul24(r - HALF_PATCH, S);
         }
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // IC's window reads before the overlay writes
-    // row pass: task = (4 window rows = 2 row pairs, group of 4 columns); window row r = level row
-    // y-21+r, sum column hc = level column x-18+hc; its 7 input bytes start at window byte
-    // x-5-xa+hc.  The sums overlay the window (Hs = window + OD_HOFF): the first 64 tasks take
-    // the lower row blocks (rq 10 .. 4), whose writes (from byte OD_HOFF + 160 * 8) only land
-    // on window rows >= 22, already read; the second round reads rows 0 .. 19 (LDS is in order
-    // per wave, and a task's reads precede its writes).
+    // row pass on the matrix cores: for M-tile m (window rows kOdRow[m] .. +15) and N-tile t
+    // (output columns n = 16t .. 16t+15 of the window), H = A x B with A = the window bytes as
+    // i8 (p ^ 0x80 = p - 128) and B = the banded tap matrix B[k][n] = tap[k - n] (c_rowB), one
+    // v_mfma_i32_16x16x64_i8 over all 64 window columns.  Columns 61 .. 63 (never inside a
+    // needed band: sum column hc reads window columns o0 + hc .. o0 + hc + 6 <= 60) carry
+    // (127, 127, 11) in A and (127, 127, 58) in B: + 32896 = 128 * 257 restores the unsigned
+    // sum, so H = sum tap * p exactly (0 .. 65535).  Lane l holds H of column 16t + (l & 15),
+    // rows kOdRow[m] + 4(l >> 4) .. +3: two row-pair dwords Hs[pair][n] (56 columns per pair
+    // row, so 8 work-groups fit a CU; the column pass adds o0).  All window reads are issued before the first write (LDS
+    // is in order per wave), so the sums overlay the window.
     {
-        const int o0 = x - 5 - xa;  // 0..15, wave-uniform
-        const int sb = o0 & 3, sd = o0 >> 2;
-        const uint32_t* W32 = (const uint32_t*)W;
-        static_assert((OD_HPR / 2) * (OD_HC / 4) == 110, "row-pass task count");
+        const int r16 = lane & 15, h4 = lane >> 4;
+        const uint4* W4 = (const uint4*)W;
+        uint4 A[3];
 #pragma unroll
-        for (int it = 0; it < 2; ++it) {
-            // tasks 110 .. 127 of the second round repeat tasks 90 .. 107 of the same round
-            // (identical values to identical addresses): no lane is masked off
-            int task = lane + 64 * it;
-            if (task >= 110) task -= 20;
-            const int rt = task / (OD_HC / 4), gq = task - rt * (OD_HC / 4);
-            const int rq = OD_HPR / 2 - 1 - rt;
-            uint32_t h[4][4];
+        for (int m = 0; m < 3; ++m) A[m] = W4[(kOdRow[m] + r16) * (OD_WP / 16) + h4];
+        const uint32_t keep = h4 == 3 ? 0x000000FFu : 0xFFFFFFFFu;
+        const uint32_t bias = h4 == 3 ? 0x0B7F7F00u : 0u;
+        const i32x4v zero = {0, 0, 0, 0};
+        uint32_t* q3 = Hs + 2 * h4 * OD_HN + r16 + (r16 >= 8 ? 32 : 48);
 #pragma unroll
-            for (int s2 = 0; s2 < 4; ++s2) {
-                const int r = min(4 * rq + s2, 2 * OD_WR);  // row 43 pads the last pair (tap 0)
-                // bytes 0 .. 9 of the span (byte 9 lies in d3 when sb == 3)
-                const uint32_t* q = W32 + r * (OD_WP / 4) + gq + sd;
-                const uint32_t d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3];
-                hrow4(__builtin_amdgcn_alignbyte(d1, d0, sb), __builtin_amdgcn_alignbyte(d2, d1, sb),
-                      __builtin_amdgcn_alignbyte(d3, d2, sb), h[s2]);
+        for (int m = 0; m < 3; ++m) {
+            i32x4v a;
+            a.x = (int)(A[m].x ^ 0x80808080u);
+            a.y = (int)(A[m].y ^ 0x80808080u);
+            a.z = (int)(A[m].z ^ 0x80808080u);
+            a.w = (int)(((A[m].w ^ 0x80808080u) & keep) | bias);
+            i32x4v c[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) c[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, Bf[t], zero, 0, 0, 0);
+            uint32_t* q = Hs + (kOdRow[m] / 2 + 2 * h4) * OD_HN + r16;
+            // N-tile 3 first: its columns 56 .. 63 (beyond the 56-column pair rows) go to the
+            // lane's own tile-2 slots, which tile 2 then overwrites (same lane, program order)
+            q3[0] = (uint32_t)c[3].x | ((uint32_t)c[3].y << 16);
+            q3[OD_HN] = (uint32_t)c[3].z | ((uint32_t)c[3].w << 16);
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+                q[16 * t] = (uint32_t)c[t].x | ((uint32_t)c[t].y << 16);
+                q[16 * t + OD_HN] = (uint32_t)c[t].z | ((uint32_t)c[t].w << 16);
             }
-#pragma unroll
-            for (int pr = 0; pr < 2; ++pr) {
-                uint4 o;
-                o.x = h[2 * pr][0] | (h[2 * pr + 1][0] << 16);
-                o.y = h[2 * pr][1] | (h[2 * pr + 1][1] << 16);
-                o.z = h[2 * pr][2] | (h[2 * pr + 1][2] << 16);
-                o.w = h[2 * pr][3] | (h[2 * pr + 1][3] << 16);
-                *(uint4*)(Hs + (2 * rq + pr) * OD_HC + 4 * gq) = o;
-            }
+            q3 += (kOdRow[m + (m < 2)] - kOdRow[m]) / 2 * OD_HN;
         }
     }
     m01 = wave_total(m01);
@@ -2055,20 +2057,57 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
     // wave-uniform: can any sample leave the ROI (raw border bytes) or reach the scalar tail?
     const bool edge = x - 18 < 0 || x + 18 >= lg.w || y - 18 < 0 || y + 18 >= lg.h;
     const bool tailAny = x + 18 >= lg.xsimd_blur;
+    const int o0 = x - 5 - xa;  // window column of sum column hc = 0 (level column x - 18)
+    // Sample offsets: dy = cvRound(fma(px, b, py * a)), dx = cvRound(fma(px, a, -(py * b)))
+    // (ORBextractor.cc:168-169 as g++ contracts them) on packed f32 pairs; cvRound = round half
+    // to even of the float, taken as the low bits of v + (1.5 * 2^23 + 18) (one more RNE
+    // rounding, exact for |v| < 2^22; the even addend keeps the tie parity), so the bits are
+    // kMagic + dy + 18 = kMagic + r0 (window row of the first tap) and kMagic + dx + 18.
+    constexpr uint32_t kMagic = 0x4B400000u;
+    typedef float f32x2v __attribute__((ext_vector_type(2)));
+    const f32x2v rA = {a, -bsin}, rB = {bsin, a};
+    // tap words of the column pass for even / odd r0, opaque so they stay in VGPRs
+    uint32_t tE0 = GP_E0, tE1 = GP_E1, tE2 = GP_E2, tE3 = GP_E3;
+    uint32_t tO0 = GP_O0, tO1 = GP_O1, tO2 = GP_O2, tO3 = GP_O3;
+    asm volatile("" : "+v"(tE0), "+v"(tE1), "+v"(tE2), "+v"(tE3), "+v"(tO0), "+v"(tO1), "+v"(tO2), "+v"(tO3));
+    // sum (pair p, column dx + 18 + o0) = hbase[56 p + bits_x] (32-bit LDS addresses wrap)
+    const uint32_t* hbase = Hs + (o0 - (int)kMagic);
+    // tail columns (scalar-tail rounding): x + dx >= xsimd_blur <=> bits_x >= thr
+    const uint32_t thr = kMagic + 18u + (uint32_t)(lg.xsimd_blur - x);
+    uint32_t bxs[8], bys[8];
     int vals[8];
+    // one copy of the loop per wave-uniform tail case (no per-sample tail test when none)
+    auto samples = [&](auto tailC) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-        const float px = pat[2 * q], py = pat[2 * q + 1];
-        const int dy = (int)rintf(__builtin_fmaf(px, bsin, py * a));
-        const int dx = (int)rintf(__builtin_fmaf(px, a, -(py * bsin)));
-        const uint32_t T = vpass(Hs, dy + OD_WR - 3, dx + 18);
-        uint32_t v = blur_round(T, tailAny && x + dx >= lg.xsimd_blur);
-        if (edge) {
-            const int X = x + dx, Y = y + dy;
-            if (X < 0 || X >= lg.w || Y < 0 || Y >= lg.h)  // the window is overlaid: the padded level itself
-                v = pyr[lg.base + (long long)b * lg.fstride + (long long)(Y + EDGE) * lg.pitch + (X + EDGE)];
+        const f32x2v pyv = {pat[2 * q + 1], pat[2 * q + 1]}, pxv = {pat[2 * q], pat[2 * q]};
+        // (the magic add per element: this compiler turns a <2 x float> add of a splat literal
+        // into the low lane's sum copied to both lanes)
+        const f32x2v R = __builtin_elementwise_fma(pxv, rB, pyv * rA);
+        const uint32_t by = __builtin_bit_cast(uint32_t, R.x + 12582930.0f);
+        const uint32_t bx = __builtin_bit_cast(uint32_t, R.y + 12582930.0f);
+        bxs[q] = bx;
+        bys[q] = by;
+        const uint32_t* hq = hbase + (int)(__umul24(__builtin_amdgcn_ubfe(by, 1, 8), OD_HN) + bx);
+        // odd r0: the first pair starts one row early (taps shifted by one u16 lane)
+        const uint32_t om = (uint32_t)__builtin_amdgcn_sbfe((int)by, 0, 1);
+        const uint32_t t0 = bfi(om, tO0, tE0), t1 = bfi(om, tO1, tE1);
+        const uint32_t t2 = bfi(om, tO2, tE2), t3 = bfi(om, tO3, tE3);
+        const uint32_t T = dot2u(hq[3 * OD_HN], t3, dot2u(hq[2 * OD_HN], t2, dot2u(hq[OD_HN], t1, dot2u(hq[0], t0, 0u))));
+        vals[q] = (int)blur_round(T, decltype(tailC)::value && bx >= thr);
+    }
+    };
+    if (tailAny)
+        samples(std::true_type{});
+    else
+        samples(std::false_type{});
+    if (edge) {  // samples outside the ROI read the padded level itself (the window is overlaid)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int X = x + (int)(bxs[q] - kMagic) - 18, Y = y + (int)(bys[q] - kMagic) - 18;
+            if (X < 0 || X >= lg.w || Y < 0 || Y >= lg.h)
+                vals[q] = pyr[lg.base + (long long)b * lg.fstride + (long long)(Y + EDGE) * lg.pitch + (X + EDGE)];
         }
-        vals[q] = (int)v;
     }
     int nib = 0;
 #pragma unroll
@@ -2759,7 +2798,7 @@ struct orb_extractor {
         gaussian_taps7(k7);
         for (int i = 0; i < 4; ++i) G.taps[i] = k7[3 + i];
         if (G.taps[0] != 55 || G.taps[1] != 49 || G.taps[2] != 34 || G.taps[3] != 18)
-            return set_err(ORB_EINVAL, "Gaussian taps differ from the kernel's constants (GT_WA/GT_WB)");
+            return set_err(ORB_EINVAL, "Gaussian taps differ from the kernel's constants (c_rowB, GP_*)");
         for (int v = 0; v < 16; ++v) G.umax[v] = umax[v];
         G.umaxNib = 0;
         for (int v = 0; v < 16; ++v) G.umaxNib |= (unsigned long long)umax[v] << (4 * v);
@@ -3505,6 +3544,19 @@ static int upload_pattern(int device) {
                 mt[320 * sh + n] = m;
             }
         HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_icmask), mt, sizeof(mt)));
+    }
+    {  // banded 7-tap row-pass matrix (GaussianBlur 7x7 sigma 2 fixed-point taps) + the bias rows
+        static const int8_t tap[7] = {18, 34, 49, 55, 49, 34, 18};
+        uint8_t bf[4 * 64 * 16];
+        for (int t = 0; t < 4; ++t)
+            for (int l = 0; l < 64; ++l)
+                for (int j = 0; j < 16; ++j) {
+                    const int k = 16 * (l >> 4) + j, n = 16 * t + (l & 15);
+                    int8_t v = (k - n >= 0 && k - n <= 6) ? tap[k - n] : 0;
+                    if (k >= 61) v = k == 63 ? 58 : 127;  // 127*127 + 127*127 + 11*58 = 128 * 257
+                    bf[(t * 64 + l) * 16 + j] = (uint8_t)v;
+                }
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_rowB), bf, sizeof(bf)));
     }
     if (device >= 0 && device < 64) uploaded[device] = true;
     return ORB_OK;
