@@ -29,16 +29,12 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {
     const float p1 = 0.9997878412794807f * k, p3 = -0.3258083974640975f * k;
     const float p5 = 0.1555786518463281f * k, p7 = -0.04432655554792128f * k;
     const float eps = (float)2.2204460492503131e-16;  // (float)DBL_EPSILON
-    float ax = fabsf(x), ay = fabsf(y), a, c, c2;
-    if (ax >= ay) {
-        c = ay / (ax + eps);
-        c2 = c * c;
-        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
-    } else {
-        c = ax / (ay + eps);
-        c2 = c * c;
-        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
-    }
+    // the two branches of the reference share one division: c = min / (max + eps)
+    const float ax = fabsf(x), ay = fabsf(y);
+    const bool ge = ax >= ay;
+    const float c = (ge ? ay : ax) / ((ge ? ax : ay) + eps), c2 = c * c;
+    const float poly = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    float a = ge ? poly : 90.f - poly;
     if (x < 0) a = 180.f - a;
     if (y < 0) a = 360.f - a;
     return a;
@@ -61,35 +57,33 @@ __device__ __forceinline__ float sincos_poly(double x, double x2, const SinCosTa
     double x4 = x2 * x2, c2 = p.c3 + x2 * p.c4, c1 = p.c0 + x2 * p.c1, x6 = x4 * x2, c = c1 + x4 * p.c2;
     return (float)(c + x6 * c2);
 }
-// Returns cos in *c, sin in *s for y in [0, 120).
+// Returns cos in *c, sin in *s for y in [0, 120).  sinf and cosf share the reduction; each
+// polynomial is evaluated once (glibc picks sin / cos polynomial by n's parity, and table
+// t1 = t0 with every cos coefficient negated: the cos polynomial negates exactly).
 __device__ __forceinline__ void glibc_sincosf(float y, float* s_out, float* c_out) {
     const SinCosTab t0 = {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0, 0x1p0,
                           -0x1.ffffffd0c621cp-2, 0x1.55553e1068f19p-5, -0x1.6c087e89a359dp-10,
                           0x1.99343027bf8c3p-16, -0x1.555545995a603p-3, 0x1.1107605230bc4p-7,
                           -0x1.994eb3774cf24p-13};
-    const SinCosTab t1 = {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0, -0x1p0,
-                          0x1.ffffffd0c621cp-2, -0x1.55553e1068f19p-5, 0x1.6c087e89a359dp-10,
-                          -0x1.99343027bf8c3p-16, -0x1.555545995a603p-3, 0x1.1107605230bc4p-7,
-                          -0x1.994eb3774cf24p-13};
     double x = y;
-    if (abstop12(y) < abstop12(0x1.921FB6p-1f)) {
-        if (abstop12(y) < abstop12(0x1p-12f)) {
-            *s_out = y;
-            *c_out = 1.0f;
-            return;
-        }
-        double x2 = x * x;
-        *s_out = sincos_poly(x, x2, t0, 0);
-        *c_out = sincos_poly(x, x2, t0, 1);
+    int n = 0;
+    if (abstop12(y) >= abstop12(0x1.921FB6p-1f)) {  // |y| >= pi/4: x = y - n pi/2
+        const double r = x * t0.hpi_inv;
+        n = ((int32_t)r + 0x800000) >> 24;
+        x = x - n * t0.hpi;
+    }
+    const double xs = ((n + 1) & 2) ? -x : x;  // x * sign[n & 3]
+    const double x2 = x * x;
+    const float S = sincos_poly(xs, x2, t0, 0);
+    float C = sincos_poly(xs, x2, t0, 1);
+    if (n & 2) C = -C;
+    if (abstop12(y) < abstop12(0x1p-12f)) {
+        *s_out = y;
+        *c_out = 1.0f;
         return;
     }
-    double r = x * t0.hpi_inv;
-    int n = ((int32_t)r + 0x800000) >> 24;
-    x = x - n * t0.hpi;
-    double sg = t0.sign[n & 3];
-    const SinCosTab& p = (n & 2) ? t1 : t0;
-    *s_out = sincos_poly(x * sg, x * x, p, n);
-    *c_out = sincos_poly(x * sg, x * x, p, n ^ 1);
+    *s_out = (n & 1) ? C : S;
+    *c_out = (n & 1) ? S : C;
 }
 
 // DescriptorDistance (ORBmatcher.cc:1794-1810): popcount of the 256-bit XOR.

@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -49,7 +50,7 @@ __device__ unsigned long long g_kftime[8];
 // Only switches that keep the output exact (sizes, register targets, timing probes) exist in
 // this translation unit; ablations that change the output are not part of the product source.
 #if defined(KL_SKIP_FAST) || defined(KL_SKIP_QUEUE) || defined(KS_SKIP_RERUN) || defined(KS_SKIP_RETAIN) || \
-    defined(KS_SKIP_LEVEL_RETAIN) || defined(KF_NOATOMIC) || defined(KM_SKIP1) || defined(KM_SKIP2)
+    defined(KS_SKIP_LEVEL_RETAIN) || defined(KF_NOATOMIC) || defined(KM_SKIP1) || defined(KM_SKIP2) || defined(PS_EXP)
 #error "wrong-output ablation switches were removed from the product source"
 #endif
 
@@ -110,6 +111,7 @@ struct Geom {
     int taps[4];       // Gaussian 7-tap fixed-point kernel, centre first: 55, 49, 34, 18
     int umax[16];
     unsigned long long umaxNib;  // umax[0..15] as 4-bit nibbles (k_orient_desc's disc mask)
+    uint32_t odDivMagic;          // k_orient_desc: ceil(2^32 / slot groups per frame) (exact division)
     LevelGeom lv[ORB_MAX_LEVELS];
 };
 
@@ -612,9 +614,6 @@ __device__ unsigned long long g_pstime[32];
 #define PS_WAVES 8  // waves per SIMD the register allocation targets (two workgroups per CU)
 #endif
 #define PS_LB 4  // level-0 units per loader lane in flight at once
-#ifndef PS_EXP  // timing experiments only (wrong output): 1 builders idle, 2 no pyramid stores, 3 no input loads
-#define PS_EXP 0
-#endif
 __global__ void __launch_bounds__(PS_THREADS) __attribute__((amdgpu_waves_per_eu(PS_WAVES)))
 k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uint8_t* __restrict__ pyr,
              const uint32_t* __restrict__ colWords, const uint4* __restrict__ rowEntries,
@@ -642,7 +641,7 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
                         const int i = i0 + k * 64 * PS_LOADERS;
                         if (i < units) {
                             const int r = (int)__umulhi((uint32_t)i, sg.u0m), u = i - r * sg.u0;
-                            pf[k] = PS_EXP == 3 ? make_uint4(r, u, 0, 0) : load_unit16(img + (long long)(lo + r) * stride + 16 * u, w0 - 16 * u, sg.align);
+                            pf[k] = load_unit16(img + (long long)(lo + r) * stride + 16 * u, w0 - 16 * u, sg.align);
                         }
                     }
 #pragma unroll
@@ -675,12 +674,12 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
     for (int n = 0; n < sg.nRounds; ++n) {
         PS_T(t1);
         const uint32_t e = idle ? 0u : rounds[n * rw + myL];
-        const int cnt = PS_EXP == 1 ? 0 : (e >> 12) & 0x3F;
+        const int cnt = (e >> 12) & 0x3F;
         // the level's row entries of this round (scalar loads: lgkmcnt, never behind stores):
         // {source row 0, source row 1 (LDS addresses), b0 << 12, b1 << 12, own ring row (LDS
         //  address, ~0u: none), padded-row offset, top mirror offset, bottom mirror offset (~0u: none)}
         const uint4* E = rowEntries + 2 * ((int)rounds[n * rw + sg.L] + (int)(e >> 18));
-        if (cnt > 0 && myL == 0 && PS_EXP != 5) {
+        if (cnt > 0 && myL == 0) {
             // padded level-0 rows from the ring (k_pyr0's copyMakeBorder), 16 B per unit
             for (int c = ql; c < nq; c += qs) {
                 const int px = 16 * c;
@@ -689,8 +688,8 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
                     const uint4 e0 = E[2 * k], e1 = E[2 * k + 1];
                     const uint8_t* R = s_ring + e0.x;
                     uint4 v;
-                    if (inner || PS_EXP == 4) {
-                        v = *(const uint4*)(R + (PS_EXP == 4 ? max(px - EDGE, 0) : px - EDGE));
+                    if (inner) {
+                        v = *(const uint4*)(R + px - EDGE);
                     } else if (px == 0) {
                         // left border: bytes R[16], R[15], .. R[1] (reflect-101 of -16 .. -1),
                         // the aligned dwords R[0..19] reversed by v_perm
@@ -721,10 +720,6 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
                             w4[q4] = word;
                         }
                         v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
-                    }
-                    if (PS_EXP == 2) {
-                        if (v.x == 0x12345678u) *(uint4*)(D + px) = v;
-                        continue;
                     }
                     *(uint4*)(D + e1.y + px) = v;
                     if (e1.z != 0xFFFFFFFFu) *(uint4*)(D + e1.z + px) = v;
@@ -811,13 +806,9 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
                         }
                     }
                     word &= live;
-                    if (PS_EXP != 2) {
-                        *(uint32_t*)(D + e1.y + 4 * q) = word;
-                        if (e1.z != 0xFFFFFFFFu) *(uint32_t*)(D + e1.z + 4 * q) = word;
-                        if (e1.w != 0xFFFFFFFFu) *(uint32_t*)(D + e1.w + 4 * q) = word;
-                    } else if (word == 0x12345678u) {
-                        *(uint32_t*)(D + 4 * q) = word;
-                    }
+                    *(uint32_t*)(D + e1.y + 4 * q) = word;
+                    if (e1.z != 0xFFFFFFFFu) *(uint32_t*)(D + e1.z + 4 * q) = word;
+                    if (e1.w != 0xFFFFFFFFu) *(uint32_t*)(D + e1.w + 4 * q) = word;
                     if (e1.x != 0xFFFFFFFFu && roi) *(uint32_t*)(s_ring + e1.x + cx) = word;
                 }
             }
@@ -1920,7 +1911,7 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
     int bid = blockIdx.y * gridDim.x + blockIdx.x;
     const int full = (gridDim.x * gridDim.y) & ~7;
     if (OD_XCD && bid < full) bid = (bid & 7) * (full >> 3) + (bid >> 3);
-    const int b = bid / gridDim.x;
+    const int b = (int)__umulhi((uint32_t)bid, g.odDivMagic);  // bid / gridDim.x (exact: bid * gridDim.x < 2^32)
     const int k = (bid - b * gridDim.x) * 4 + wave;  // slot: level l owns [kpBase_l, kpBase_l + nDesired_l)
     int l = 0;
     for (int i = 1; i < g.L; ++i)
@@ -1929,10 +1920,13 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
     const int idx = k - lg.kpBase;
     // wave-uniform record: x, y and the window base live in SGPRs
     const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane((int)(k < g.kpCap ? lvlOut[(long long)b * g.kpCap + k] : 0u));
-    // output position: level-major order (ORBextractor.cc:749-778)
+    // output position: level-major order (ORBextractor.cc:749-778).  (Measured no faster: the
+    // counts unrolled over ORB_MAX_LEVELS in one scalar load, 0.487 vs 0.465 ms; as a per-lane
+    // vector load with a DPP prefix sum, 0.474 vs 0.470: the prologue's latency is hidden.)
+    const int* lc = lvlCount + (long long)b * g.L;
     int before = 0, cntL = 0, total = 0;
     for (int i = 0; i < g.L; ++i) {
-        const int c = lvlCount[(long long)b * g.L + i];
+        const int c = lc[i];
         before += i < l ? c : 0;
         cntL = i == l ? c : cntL;
         total += c;
@@ -3020,6 +3014,12 @@ struct orb_extractor {
         G.nCells = (int)cl.size();
         G.candPerFrame = cand;
         G.kpCap = kpCap;
+        {  // k_orient_desc's grid is ((kpCap + 3) / 4, B): bid / gridDim.x by multiply-high
+            const unsigned long long gx = (unsigned long long)(std::max(kpCap, 1) + 3) / 4;
+            G.odDivMagic = (uint32_t)(((1ull << 32) + gx - 1) / gx);
+            if (gx * gx * (unsigned long long)maxBatch >= (1ull << 32))
+                return set_err(ORB_ENOTSUP, "keypoint grid too large for k_orient_desc's block decode");
+        }
         // workspace
         // + slack: k_orient_desc's 64-byte window rows may over-read the last row's pitch
         HIP_TRY(hipMalloc(&d_pyr, (size_t)pyrBytes + 256));
