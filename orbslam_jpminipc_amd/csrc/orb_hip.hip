@@ -1943,6 +1943,7 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
     const uint32_t pu = (uint32_t)lg.pitch >> 4;
     uint8_t* W = s_buf[wave];
     uint32_t* Hs = (uint32_t*)s_buf[wave];
+    uint32_t icm[5];  // IC_Angle disc masks of the patch dwords this lane reads
     i32x4v Bf[4];  // the row pass's B fragments (constant; in flight with the window loads)
 #pragma unroll
     for (int t = 0; t < 4; ++t) Bf[t] = __builtin_bit_cast(i32x4v, c_rowB[t * 64 + lane]);
@@ -1954,6 +1955,9 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
             const int i = lane + 64 * j, r = i >> 2, c = i & 3;
             v[j] = src[i < NU ? __umul24((uint32_t)r, pu) + c : 0u];
         }
+        // the IC disc masks of this alignment, in flight with the window
+#pragma unroll
+        for (int j = 0; j < 5; ++j) icm[j] = c_icmask[320 * ((x + 1 - xa) & 3) + lane + 64 * j];
         // all 192 units stored (units >= 172 repeat unit 0 into the buffer's unused tail,
         // before the row-pass sums are written): no masked store
 #pragma unroll
@@ -1973,14 +1977,13 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
         const int pc = x + 1 - xa;  // window column of patch column u = -15
         const int pd0 = pc >> 2, sh = pc & 3;
         const uint32_t* W32 = (const uint32_t*)W;
-        const uint32_t* mt = c_icmask + 320 * sh;
         // five full 64-lane steps: dwords n >= 279 (patch rows 31 .. 35, still inside the
         // 43-row window) carry zero masks, so no lane is masked off
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
             const int n = lane + 64 * j;
             const int r = n / 9, c = n - r * 9;
-            const uint32_t pm = W32[(r + OD_WR - HALF_PATCH) * (OD_WP / 4) + pd0 + c] & mt[n];
+            const uint32_t pm = W32[(r + OD_WR - HALF_PATCH) * (OD_WP / 4) + pd0 + c] & icm[j];
             const int S = (int)__builtin_amdgcn_udot4(pm, 0x01010101u, 0u, false);
             const int T = (int)__builtin_amdgcn_udot4(pm, 0x03020100u, 0u, false);
             m10 += __mul24(4 * c - sh - HALF_PATCH, S) + T;  // 24-bit multiplies: full-rate VALU
@@ -2030,15 +2033,8 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
             q3 += (kOdRow[m + (m < 2)] - kOdRow[m]) / 2 * OD_HN;
         }
     }
-    m01 = wave_total(m01);
-    m10 = wave_total(m10);
-    const float angle = fast_atan2((float)m01, (float)m10);
-    // computeOrbDescriptor (ORBextractor.cc:155-194)
-    const float factorPI = (float)(3.14159265358979323846 / 180.f);
-    float sa, ca;
-    glibc_sincosf(angle * factorPI, &sa, &ca);
-    const float a = ca, bsin = sa;
-    float pat[16];  // pattern points 8*lane .. 8*lane+7 (tests 4*lane .. 4*lane+3): 4 float4 loads
+    float pat[16];  // pattern points 8*lane .. 8*lane+7 (tests 4*lane .. 4*lane+3): 4 float4 loads,
+                    // in flight during the angle arithmetic
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const float4 f = ((const float4*)c_patternf)[lane * 4 + q];
@@ -2047,6 +2043,14 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
         pat[4 * q + 2] = f.z;
         pat[4 * q + 3] = f.w;
     }
+    m01 = wave_total(m01);
+    m10 = wave_total(m10);
+    const float angle = fast_atan2((float)m01, (float)m10);
+    // computeOrbDescriptor (ORBextractor.cc:155-194)
+    const float factorPI = (float)(3.14159265358979323846 / 180.f);
+    float sa, ca;
+    glibc_sincosf(angle * factorPI, &sa, &ca);
+    const float a = ca, bsin = sa;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the row-pass sums are in LDS
     // wave-uniform: can any sample leave the ROI (raw border bytes) or reach the scalar tail?
     const bool edge = x - 18 < 0 || x + 18 >= lg.w || y - 18 < 0 || y + 18 >= lg.h;
