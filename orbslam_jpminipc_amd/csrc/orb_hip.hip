@@ -1905,6 +1905,8 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
                                                      const float* __restrict__ lvlResp) {
     // per wave: the raw window, then (overlaid) the row-pass sums
     __shared__ __attribute__((aligned(16))) uint8_t s_buf[4][OD_BUF];
+    __shared__ int2 s_mom[4];     // the waves' IC moments (m01, m10)
+    __shared__ float4 s_trig[4];  // angle, sin, cos of the waves' keypoints
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     // XCD-aware block order: workgroup i runs on XCD i % 8, so give each XCD a contiguous run
     // of keypoints (neighbouring keypoints share window rows: L2 hits instead of HBM re-reads)
@@ -1932,7 +1934,8 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
         total += c;
     }
     if (k == 0 && lane == 0) counts[b] = total;
-    if (k >= g.kpCap || idx >= cntL) return;  // wave-uniform
+    // an empty slot's wave does no work but stays for the workgroup's two barriers
+    const bool active = k < g.kpCap && idx < cntL;  // wave-uniform
     const int x = e & 0xFFF, y = (e >> 12) & 0xFFF, score = e >> 24;
     // raw window: padded rows y-5 .. y+37 (level rows y-21 .. y+21), padded columns xa .. xa+63
     // (inside the padded frame: 16 <= x <= w-7 and y likewise, App. B / DESIGN §4; the last
@@ -1947,7 +1950,7 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
     i32x4v Bf[4];  // the row pass's B fragments (constant; in flight with the window loads)
 #pragma unroll
     for (int t = 0; t < 4; ++t) Bf[t] = __builtin_bit_cast(i32x4v, c_rowB[t * 64 + lane]);
-    {
+    if (active) {
         constexpr int NU = (2 * OD_WR + 1) * 4;  // 172 16-byte units
         uint4 v[3];
 #pragma unroll
@@ -1966,14 +1969,14 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
             ((uint4*)W)[(i >> 2) * (OD_WP / 16) + (i & 3)] = v[j];
         }
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS is in order per wave; compiler fence
+    if (active) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS is in order per wave; compiler fence
     // IC_Angle (ORBextractor.cc:124-151): the disc sums m10 = sum u*I, m01 = sum v*I over
     // |u| <= umax[|v|], one patch dword per lane and step (patch row v = window row v + 21,
     // patch dword c = window dword pd0 + c).  Byte i of dword c sits at u = base + i,
     // base = 4c - sh - 15, so a dword adds base * S + sum(i * I_i) to m10 and v * S to m01,
     // S = its in-disc byte sum: two v_dot4 on the masked dword (integer sums: any order).
     int m01 = 0, m10 = 0;
-    {
+    if (active) {
         const int pc = x + 1 - xa;  // window column of patch column u = -15
         const int pd0 = pc >> 2, sh = pc & 3;
         const uint32_t* W32 = (const uint32_t*)W;
@@ -1990,6 +1993,22 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
             m01 += __mul24(r - HALF_PATCH, S);
         }
     }
+    // IC_Angle's sums, then the angle arithmetic (fastAtan2, glibc sincosf: ~100 VALU, a fifth of a
+    // keypoint's) once per workgroup: wave 0's lanes 0 .. 3 for the four slots, between the
+    // two barriers, while the other waves run their row passes
+    m01 = wave_total(m01);
+    m10 = wave_total(m10);
+    if (lane == 0) s_mom[wave] = make_int2(m01, m10);
+    lds_barrier();
+    if (wave == 0 && lane < 4) {
+        const int2 mm = s_mom[lane];
+        const float ang = fast_atan2((float)mm.x, (float)mm.y);
+        // computeOrbDescriptor (ORBextractor.cc:155-194)
+        const float factorPI = (float)(3.14159265358979323846 / 180.f);
+        float sa, ca;
+        glibc_sincosf(ang * factorPI, &sa, &ca);
+        s_trig[lane] = make_float4(ang, sa, ca, 0.f);
+    }
     // row pass on the matrix cores: for M-tile m (window rows kOdRow[m] .. +15) and N-tile t
     // (output columns n = 16t .. 16t+15 of the window), H = A x B with A = the window bytes as
     // i8 (p ^ 0x80 = p - 128) and B = the banded tap matrix B[k][n] = tap[k - n] (c_rowB), one
@@ -2000,7 +2019,7 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
     // rows kOdRow[m] + 4(l >> 4) .. +3: two row-pair dwords Hs[pair][n] (56 columns per pair
     // row, so 8 work-groups fit a CU; the column pass adds o0).  All window reads are issued before the first write (LDS
     // is in order per wave), so the sums overlay the window.
-    {
+    if (active) {
         const int r16 = lane & 15, h4 = lane >> 4;
         const uint4* W4 = (const uint4*)W;
         uint4 A[3];
@@ -2034,7 +2053,7 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
         }
     }
     float pat[16];  // pattern points 8*lane .. 8*lane+7 (tests 4*lane .. 4*lane+3): 4 float4 loads,
-                    // in flight during the angle arithmetic
+                    // in flight across the second barrier
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const float4 f = ((const float4*)c_patternf)[lane * 4 + q];
@@ -2043,14 +2062,10 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
         pat[4 * q + 2] = f.z;
         pat[4 * q + 3] = f.w;
     }
-    m01 = wave_total(m01);
-    m10 = wave_total(m10);
-    const float angle = fast_atan2((float)m01, (float)m10);
-    // computeOrbDescriptor (ORBextractor.cc:155-194)
-    const float factorPI = (float)(3.14159265358979323846 / 180.f);
-    float sa, ca;
-    glibc_sincosf(angle * factorPI, &sa, &ca);
-    const float a = ca, bsin = sa;
+    lds_barrier();  // s_trig is written (and the row-pass sums: LDS)
+    if (!active) return;
+    const float4 trig = s_trig[wave];
+    const float angle = trig.x, a = trig.z, bsin = trig.y;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the row-pass sums are in LDS
     // wave-uniform: can any sample leave the ROI (raw border bytes) or reach the scalar tail?
     const bool edge = x - 18 < 0 || x + 18 >= lg.w || y - 18 < 0 || y + 18 >= lg.h;
