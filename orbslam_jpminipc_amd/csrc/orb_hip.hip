@@ -1915,31 +1915,21 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
     if (OD_XCD && bid < full) bid = (bid & 7) * (full >> 3) + (bid >> 3);
     const int b = (int)__umulhi((uint32_t)bid, g.odDivMagic);  // bid / gridDim.x (exact: bid * gridDim.x < 2^32)
     const int k = (bid - b * gridDim.x) * 4 + wave;  // slot: level l owns [kpBase_l, kpBase_l + nDesired_l)
+    // wave-uniform record: x, y and the window base live in SGPRs (its load first: the window's
+    // address depends on it)
+    const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane((int)lvlOut[(long long)b * g.kpCap + min(k, g.kpCap - 1)]);
     int l = 0;
     for (int i = 1; i < g.L; ++i)
         if (k >= g.lv[i].kpBase) l = i;
     const LevelGeom& lg = g.lv[l];
     const int idx = k - lg.kpBase;
-    // wave-uniform record: x, y and the window base live in SGPRs
-    const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane((int)(k < g.kpCap ? lvlOut[(long long)b * g.kpCap + k] : 0u));
-    // output position: level-major order (ORBextractor.cc:749-778).  (Measured no faster: the
-    // counts unrolled over ORB_MAX_LEVELS in one scalar load, 0.487 vs 0.465 ms; as a per-lane
-    // vector load with a DPP prefix sum, 0.474 vs 0.470: the prologue's latency is hidden.)
-    const int* lc = lvlCount + (long long)b * g.L;
-    int before = 0, cntL = 0, total = 0;
-    for (int i = 0; i < g.L; ++i) {
-        const int c = lc[i];
-        before += i < l ? c : 0;
-        cntL = i == l ? c : cntL;
-        total += c;
-    }
-    if (k == 0 && lane == 0) counts[b] = total;
-    // an empty slot's wave does no work but stays for the workgroup's two barriers
-    const bool active = k < g.kpCap && idx < cntL;  // wave-uniform
-    const int x = e & 0xFFF, y = (e >> 12) & 0xFFF, score = e >> 24;
     // raw window: padded rows y-5 .. y+37 (level rows y-21 .. y+21), padded columns xa .. xa+63
-    // (inside the padded frame: 16 <= x <= w-7 and y likewise, App. B / DESIGN §4; the last
-    // row's over-read stays inside the pyramid's tail slack)
+    // (keypoints lie in 16 <= x <= w-7 and y likewise, App. B / DESIGN §4; the clamp only keeps
+    // an empty slot's stale record inside the level; the last row's over-read stays inside the
+    // pyramid's tail slack).  Loaded before the slot is known to be filled: the per-level counts
+    // are scalar loads of their own
+    const int x = min(max((int)(e & 0xFFF), 16), lg.w - 7), y = min(max((int)((e >> 12) & 0xFFF), 16), lg.h - 7);
+    const int score = e >> 24;
     const int xa = (x - 5) & ~15;
     const uint4* src = (const uint4*)(pyr + lg.base + (long long)b * lg.fstride +
                                       (long long)(y + EDGE - OD_WR) * lg.pitch + xa);
@@ -1950,17 +1940,17 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
     i32x4v Bf[4];  // the row pass's B fragments (constant; in flight with the window loads)
 #pragma unroll
     for (int t = 0; t < 4; ++t) Bf[t] = __builtin_bit_cast(i32x4v, c_rowB[t * 64 + lane]);
-    if (active) {
-        constexpr int NU = (2 * OD_WR + 1) * 4;  // 172 16-byte units
-        uint4 v[3];
+    constexpr int NU = (2 * OD_WR + 1) * 4;  // 172 16-byte units
+    uint4 v[3];
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            const int i = lane + 64 * j, r = i >> 2, c = i & 3;
-            v[j] = src[i < NU ? __umul24((uint32_t)r, pu) + c : 0u];
-        }
-        // the IC disc masks of this alignment, in flight with the window
+    for (int j = 0; j < 3; ++j) {
+        const int i = lane + 64 * j, r = i >> 2, c = i & 3;
+        v[j] = src[i < NU ? __umul24((uint32_t)r, pu) + c : 0u];
+    }
+    // the IC disc masks of this alignment, in flight with the window
 #pragma unroll
-        for (int j = 0; j < 5; ++j) icm[j] = c_icmask[320 * ((x + 1 - xa) & 3) + lane + 64 * j];
+    for (int j = 0; j < 5; ++j) icm[j] = c_icmask[320 * ((x + 1 - xa) & 3) + lane + 64 * j];
+    {
         // all 192 units stored (units >= 172 repeat unit 0 into the buffer's unused tail,
         // before the row-pass sums are written): no masked store
 #pragma unroll
@@ -1969,14 +1959,14 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
             ((uint4*)W)[(i >> 2) * (OD_WP / 16) + (i & 3)] = v[j];
         }
     }
-    if (active) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS is in order per wave; compiler fence
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS is in order per wave; compiler fence
     // IC_Angle (ORBextractor.cc:124-151): the disc sums m10 = sum u*I, m01 = sum v*I over
     // |u| <= umax[|v|], one patch dword per lane and step (patch row v = window row v + 21,
     // patch dword c = window dword pd0 + c).  Byte i of dword c sits at u = base + i,
     // base = 4c - sh - 15, so a dword adds base * S + sum(i * I_i) to m10 and v * S to m01,
     // S = its in-disc byte sum: two v_dot4 on the masked dword (integer sums: any order).
     int m01 = 0, m10 = 0;
-    if (active) {
+    {
         const int pc = x + 1 - xa;  // window column of patch column u = -15
         const int pd0 = pc >> 2, sh = pc & 3;
         const uint32_t* W32 = (const uint32_t*)W;
@@ -1993,6 +1983,19 @@ __global__ void __launch_bounds__(256) k_orient_desc(const uint8_t* __restrict__
             m01 += __mul24(r - HALF_PATCH, S);
         }
     }
+    // output position: level-major order (ORBextractor.cc:749-778); after the window and IC
+    // (scalar loads of the frame's counts: a loop ahead of the window loads delayed them)
+    const int* lc = lvlCount + (long long)b * g.L;
+    int before = 0, cntL = 0, total = 0;
+    for (int i = 0; i < g.L; ++i) {
+        const int c = lc[i];
+        before += i < l ? c : 0;
+        cntL = i == l ? c : cntL;
+        total += c;
+    }
+    if (k == 0 && lane == 0) counts[b] = total;
+    // an empty slot's wave does no work but stays for the workgroup's two barriers
+    const bool active = k < g.kpCap && idx < cntL;  // wave-uniform
     // IC_Angle's sums, then the angle arithmetic (fastAtan2, glibc sincosf: ~100 VALU, a fifth of a
     // keypoint's) once per workgroup: wave 0's lanes 0 .. 3 for the four slots, between the
     // two barriers, while the other waves run their row passes
