@@ -2426,89 +2426,106 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
     __syncthreads();
     KM_T(3);
     // ---- phase 2: the sequential greedy pass (ORBmatcher.cc:611-680) on one wave ----
-    // Per query the critical path is one LDS read of its top-8 slots' state and scalar lane
-    // reads (v_readlane: no LDS round trip); the next query's list is fetched while this one
-    // resolves, and the rotation bins are computed afterwards, in parallel (phase 3).
+    // Speculated eight queries at a time (lane 8g + c: query q0 + g, candidate c of its top-8),
+    // exact: query q reads only the states of its first min(cnt, 8) slots, and an accepted query
+    // changes exactly one slot (its best).  So every query of the batch is decided from the
+    // batch-start state unless an earlier query of the batch accepted a slot in its top-8, or it
+    // needs the window rescan (a truncated top-8 with < 2 live candidates); the batch commits
+    // its queries before the first such one (their slots are distinct, their vnMatches21
+    // predecessors precede the batch) and the next batch starts there.  A rescan query heading
+    // a batch runs alone on the whole wave.
     if (wave == 0 && n1c > 0) {
-        int cntN = s_lcnt[0], i1N = s_q2i[0];
-        uint32_t eN = lane < MATCH_TOPK ? s_list[lane] : 0xFFFFFFFFu;
-        for (int q = 0; q < n1c; ++q) {
-            const int cnt = cntN, i1 = i1N;
-            const uint32_t e = eN;
-            if (q + 1 < n1c) {
-                cntN = s_lcnt[q + 1];
-                i1N = s_q2i[q + 1];
-                eN = lane < MATCH_TOPK ? s_list[(q + 1) * MATCH_TOPK + lane] : 0xFFFFFFFFu;
-            }
-            if (cnt == 0) continue;  // vIndices2.empty()
+        const int grp = lane >> 3, cand = lane & 7;
+        int q0 = 0;
+        while (q0 < n1c) {
+            const int q = q0 + grp;
+            const bool qin = q < n1c;
+            const int cnt = qin ? s_lcnt[q] : 0;
             const int k = min(cnt, MATCH_TOPK);
-            const uint2 st = lane < k ? s_st[e & SLOT] : make_uint2(0u, 0u);
-            const bool valid = lane < k && (int)(st.x & 0xFFFFu) > (int)(e >> KB);
-            const uint64_t m = __ballot(valid);
-            uint32_t best, bst, bidx;
-            int second;
-            if (__popcll(m) >= 2 || cnt <= MATCH_TOPK) {
-                if (m == 0) continue;  // every candidate already held at <= its distance
-                const int e1 = __ffsll((unsigned long long)m) - 1;
-                best = (uint32_t)__builtin_amdgcn_readlane((int)e, e1);
-                bst = (uint32_t)__builtin_amdgcn_readlane((int)st.x, e1);
-                bidx = (uint32_t)__builtin_amdgcn_readlane((int)st.y, e1);
-                const uint64_t m2 = m & (m - 1);
-                second = m2 ? (int)((uint32_t)__builtin_amdgcn_readlane((int)e, __ffsll((unsigned long long)m2) - 1) >> KB)
-                            : 0x7fffffff;
-            } else {
-                // exact rescan of the whole window
-                const float qx = s_qx[q], qy = s_qy[q];
-                const int minCX = max(0, (int)floorf((qx - mg.minX - r) * mg.invW));
-                const int maxCX = min(63, (int)ceilf((qx - mg.minX + r) * mg.invW));
-                const int minCY = max(0, (int)floorf((qy - mg.minY - r) * mg.invH));
-                const int maxCY = min(47, (int)ceilf((qy - mg.minY + r) * mg.invH));
-                uint32_t d1[8];
+            const uint32_t e = cand < k ? s_list[q * MATCH_TOPK + cand] : 0xFFFFFFFFu;
+            const uint2 st = cand < k ? s_st[e & SLOT] : make_uint2(0u, 0u);
+            const bool valid = cand < k && (int)(st.x & 0xFFFFu) > (int)(e >> KB);
+            const uint32_t gm = (uint32_t)(__ballot(valid) >> (8 * grp)) & 0xFFu;
+            const bool rescan = cnt > MATCH_TOPK && __popc(gm) < 2;
+            // the group's best (first live candidate: the lists are sorted) and second
+            const int e1 = gm ? __ffs(gm) - 1 : 0;
+            const uint32_t gm2 = gm & (gm - 1u);
+            const int e2 = gm2 ? __ffs(gm2) - 1 : 0;
+            const uint32_t best = (uint32_t)__shfl((int)e, 8 * grp + e1, 64);
+            const uint32_t bst = (uint32_t)__shfl((int)st.x, 8 * grp + e1, 64);
+            const uint32_t bidx = (uint32_t)__shfl((int)st.y, 8 * grp + e1, 64);
+            const uint32_t sec = (uint32_t)__shfl((int)e, 8 * grp + e2, 64);
+            const int second = gm2 ? (int)(sec >> KB) : 0x7fffffff;
+            const int bestDist = (int)(best >> KB), bestSlot = (int)(best & SLOT);
+            const bool accept = gm != 0u && !rescan && bestDist <= 50 && (float)bestDist < (float)second * nnratio;
+            // first query the batch-start state cannot decide
+            const uint64_t accM = __ballot(accept && cand == 0);  // bit 8g: group g accepts
+            bool hit = false;
 #pragma unroll
-                for (int w = 0; w < 8; ++w) d1[w] = D1[(long long)i1 * 8 + w];
-                uint32_t lb = 0xFFFFFFFFu;
-                int ls = 0x7fffffff;
-                const int j1 = s_col[max(maxCX + 1, 0)];
-                for (int j = s_col[min(minCX, 64)] + lane; j < j1; j += 64) {
-                    const int cell = s_cell[j];
-                    const int cx = cell / 48, cy = cell - cx * 48;
-                    if (cx < minCX || cx > maxCX || cy < minCY || cy > maxCY) continue;
-                    if (fabsf(s_x2[j] - qx) > r || fabsf(s_y2[j] - qy) > r) continue;
-                    const int dist = hamming256(d1, s_d2 + j * 8);
-                    if ((int)(s_st[j].x & 0xFFFFu) <= dist) continue;
-                    const uint32_t key = ((uint32_t)dist << KB) | (uint32_t)j;
-                    if (key < lb) {
-                        if (lb != 0xFFFFFFFFu) ls = (int)(lb >> KB);
-                        lb = key;
-                    } else if (dist < ls) {
-                        ls = dist;
-                    }
-                }
-                uint32_t gb = lb;
-#pragma unroll
-                for (int o = 32; o >= 1; o >>= 1) gb = min(gb, (uint32_t)__shfl_xor((int)gb, o, 64));
-                if (gb == 0xFFFFFFFFu) continue;
-                int contrib = (lb == gb) ? ls : (lb == 0xFFFFFFFFu ? 0x7fffffff : (int)(lb >> KB));
-#pragma unroll
-                for (int o = 32; o >= 1; o >>= 1) contrib = min(contrib, __shfl_xor(contrib, o, 64));
-                best = gb;
-                second = contrib;
-                const uint2 sb = s_st[gb & SLOT];
-                bst = sb.x;
-                bidx = sb.y;
+            for (int g2 = 0; g2 < 7; ++g2) {
+                if (!((accM >> (8 * g2)) & 1ull)) continue;  // wave-uniform
+                const int bs = __builtin_amdgcn_readlane(bestSlot, 8 * g2);
+                hit = hit || (grp > g2 && cand < k && (int)(e & SLOT) == bs);
             }
-            const int bestDist = (int)(best >> KB);
-            const int bestSlot = (int)(best & SLOT);
-            if (bestDist <= 50 && (float)bestDist < (float)second * nnratio) {
-                // one wave: its LDS accesses complete in issue order, so lane 0's writes are
-                // seen by the next query's reads
-                if (lane == 0) {
-                    const int old = (int)(bst >> 16) - 1;  // vnMatches21[bestIdx2]
-                    if (old >= 0) s_m12[old] = -1;
-                    s_m12[i1] = (int)bidx;
-                    s_st[bestSlot].x = (uint32_t)bestDist | ((uint32_t)(i1 + 1) << 16);
-                    s_bslot[i1] = (short)bestSlot;
+            const uint64_t stopM = __ballot(hit || (rescan && cand == 0));
+            const int jstop = stopM ? (__ffsll((unsigned long long)stopM) - 1) >> 3 : 8;
+            if (accept && cand == 0 && grp < jstop) {
+                // distinct slots: these writes commute; the next batch's reads follow them
+                const int i1 = s_q2i[q];
+                const int old = (int)(bst >> 16) - 1;  // vnMatches21[bestIdx2]
+                if (old >= 0) s_m12[old] = -1;
+                s_m12[i1] = (int)bidx;
+                s_st[bestSlot].x = (uint32_t)bestDist | ((uint32_t)(i1 + 1) << 16);
+                s_bslot[i1] = (short)bestSlot;
+            }
+            if (jstop > 0) {
+                q0 += jstop;
+                continue;
+            }
+            // query q0 needs the exact rescan of its whole window, on all 64 lanes
+            const int i1 = s_q2i[q0];
+            const float qx = s_qx[q0], qy = s_qy[q0];
+            const int minCX = max(0, (int)floorf((qx - mg.minX - r) * mg.invW));
+            const int maxCX = min(63, (int)ceilf((qx - mg.minX + r) * mg.invW));
+            const int minCY = max(0, (int)floorf((qy - mg.minY - r) * mg.invH));
+            const int maxCY = min(47, (int)ceilf((qy - mg.minY + r) * mg.invH));
+            uint32_t d1[8];
+#pragma unroll
+            for (int w = 0; w < 8; ++w) d1[w] = D1[(long long)i1 * 8 + w];
+            uint32_t lb = 0xFFFFFFFFu;
+            int ls = 0x7fffffff;
+            const int j1 = s_col[max(maxCX + 1, 0)];
+            for (int j = s_col[min(minCX, 64)] + lane; j < j1; j += 64) {
+                const int cell = s_cell[j];
+                const int cx = cell / 48, cy = cell - cx * 48;
+                if (cx < minCX || cx > maxCX || cy < minCY || cy > maxCY) continue;
+                if (fabsf(s_x2[j] - qx) > r || fabsf(s_y2[j] - qy) > r) continue;
+                const int dist = hamming256(d1, s_d2 + j * 8);
+                if ((int)(s_st[j].x & 0xFFFFu) <= dist) continue;
+                const uint32_t key = ((uint32_t)dist << KB) | (uint32_t)j;
+                if (key < lb) {
+                    if (lb != 0xFFFFFFFFu) ls = (int)(lb >> KB);
+                    lb = key;
+                } else if (dist < ls) {
+                    ls = dist;
                 }
+            }
+            uint32_t gb = lb;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) gb = min(gb, (uint32_t)__shfl_xor((int)gb, o, 64));
+            int contrib = (lb == gb) ? ls : (lb == 0xFFFFFFFFu ? 0x7fffffff : (int)(lb >> KB));
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) contrib = min(contrib, __shfl_xor(contrib, o, 64));
+            q0 += 1;
+            if (gb == 0xFFFFFFFFu) continue;
+            const int rDist = (int)(gb >> KB), rSlot = (int)(gb & SLOT);
+            if (rDist <= 50 && (float)rDist < (float)contrib * nnratio && lane == 0) {
+                const uint2 sb = s_st[rSlot];
+                const int old = (int)(sb.x >> 16) - 1;
+                if (old >= 0) s_m12[old] = -1;
+                s_m12[i1] = (int)sb.y;
+                s_st[rSlot].x = (uint32_t)rDist | ((uint32_t)(i1 + 1) << 16);
+                s_bslot[i1] = (short)rSlot;
             }
         }
     }
