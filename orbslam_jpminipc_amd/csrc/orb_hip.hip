@@ -2206,6 +2206,12 @@ __device__ unsigned long long g_kmtime[8];
 #else
 #define KM_T(i)
 #endif
+// Minimum over each aligned group of 8 lanes (DPP: quad_perm xor 1, xor 2, row_half_mirror).
+__device__ __forceinline__ uint32_t min8(uint32_t v) {
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));
+    return min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false));
+}
 __device__ __forceinline__ void topk_insert(uint32_t (&t)[MATCH_TOPK], uint32_t key) {
 #pragma unroll
     for (int i = 0; i < MATCH_TOPK; ++i) {
@@ -2445,19 +2451,17 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
             const uint32_t e = cand < k ? s_list[q * MATCH_TOPK + cand] : 0xFFFFFFFFu;
             const uint2 st = cand < k ? s_st[e & SLOT] : make_uint2(0u, 0u);
             const bool valid = cand < k && (int)(st.x & 0xFFFFu) > (int)(e >> KB);
-            const uint32_t gm = (uint32_t)(__ballot(valid) >> (8 * grp)) & 0xFFu;
-            const bool rescan = cnt > MATCH_TOPK && __popc(gm) < 2;
-            // the group's best (first live candidate: the lists are sorted) and second
-            const int e1 = gm ? __ffs(gm) - 1 : 0;
-            const uint32_t gm2 = gm & (gm - 1u);
-            const int e2 = gm2 ? __ffs(gm2) - 1 : 0;
-            const uint32_t best = (uint32_t)__shfl((int)e, 8 * grp + e1, 64);
-            const uint32_t bst = (uint32_t)__shfl((int)st.x, 8 * grp + e1, 64);
-            const uint32_t bidx = (uint32_t)__shfl((int)st.y, 8 * grp + e1, 64);
-            const uint32_t sec = (uint32_t)__shfl((int)e, 8 * grp + e2, 64);
-            const int second = gm2 ? (int)(sec >> KB) : 0x7fffffff;
+            // the group's best (smallest live key: the lists are sorted) and second, by 8-lane
+            // min reductions on DPP (quad_perm xor 1, xor 2, row_half_mirror); the best lane
+            // keeps its own slot state for the commit
+            const uint32_t key = valid ? e : 0xFFFFFFFFu;
+            const uint32_t best = min8(key);
+            const uint32_t sec = min8(valid && e != best ? e : 0xFFFFFFFFu);
+            const bool rescan = cnt > MATCH_TOPK && sec == 0xFFFFFFFFu;  // < 2 live in a truncated list
+            const int second = sec != 0xFFFFFFFFu ? (int)(sec >> KB) : 0x7fffffff;
             const int bestDist = (int)(best >> KB), bestSlot = (int)(best & SLOT);
-            const bool accept = gm != 0u && !rescan && bestDist <= 50 && (float)bestDist < (float)second * nnratio;
+            const bool accept = best != 0xFFFFFFFFu && !rescan && bestDist <= 50 &&
+                                (float)bestDist < (float)second * nnratio;
             // first query the batch-start state cannot decide
             const uint64_t accM = __ballot(accept && cand == 0);  // bit 8g: group g accepts
             bool hit = false;
@@ -2469,12 +2473,13 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
             }
             const uint64_t stopM = __ballot(hit || (rescan && cand == 0));
             const int jstop = stopM ? (__ffsll((unsigned long long)stopM) - 1) >> 3 : 8;
-            if (accept && cand == 0 && grp < jstop) {
-                // distinct slots: these writes commute; the next batch's reads follow them
+            if (accept && valid && e == best && grp < jstop) {
+                // by the best candidate's lane; distinct slots: these writes commute, and the
+                // next batch's reads follow them
                 const int i1 = s_q2i[q];
-                const int old = (int)(bst >> 16) - 1;  // vnMatches21[bestIdx2]
+                const int old = (int)(st.x >> 16) - 1;  // vnMatches21[bestIdx2]
                 if (old >= 0) s_m12[old] = -1;
-                s_m12[i1] = (int)bidx;
+                s_m12[i1] = (int)st.y;
                 s_st[bestSlot].x = (uint32_t)bestDist | ((uint32_t)(i1 + 1) << 16);
                 s_bslot[i1] = (short)bestSlot;
             }
