@@ -2174,7 +2174,7 @@ struct MatchGeom {
     float invW, invH;  // FRAME_GRID_COLS / (maxX - minX), FRAME_GRID_ROWS / (maxY - minY)
 };
 
-// One workgroup (4 waves) per frame pair.
+// One workgroup (KM_THREADS = 8 waves) per frame pair.
 //   phase 0  F2's octave-0, in-grid keypoints — the only possible candidates of
 //            GetFeaturesInArea(x, y, window, 0, 0) (Frame.cc:200-265) — are staged,
 //            ranked by grid-traversal order (ix, iy, index: Frame.cc:233-258), so a slot
@@ -2196,6 +2196,7 @@ struct MatchGeom {
 //            descriptors / coordinates / top-8 lists live in the pair's global scratch slot
 //            (L2-resident); up to 8192 keypoints per frame.
 #define MATCH_TOPK 8
+#define KM_THREADS 512  // one workgroup (8 waves) per pair: at most a few pairs share a CU
 #define MATCH_BIG_NMAX 8192
 #ifndef KM_TIMING  // 1: per-phase s_memrealtime sums of k_match_init's pairs (experiment builds only)
 #define KM_TIMING 0
@@ -2310,14 +2311,14 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
     // ---- phase 0: keys in parallel, then ordered compaction ----
     // s_key[i2] = traversal key of F2 keypoint i2 or ~0 (not octave 0 / outside the grid);
     // s_m12[i1] = 1 if F1 keypoint i1 is a query (octave 0), as scratch.
-    for (int i = tid; i < n2; i += 256) {
+    for (int i = tid; i < n2; i += KM_THREADS) {
         const orb_keypoint_t kp = K2[i];
         const int px = (int)roundf((kp.x - mg.minX) * mg.invW);
         const int py = (int)roundf((kp.y - mg.minY) * mg.invH);
         const bool ok = kp.octave == 0 && !(px < 0 || px >= 64 || py < 0 || py >= 48);
         s_key[i] = ok ? (((uint32_t)(px * 48 + py) << 16) | (uint32_t)i) : 0xFFFFFFFFu;
     }
-    for (int i = tid; i < n1; i += 256) s_m12[i] = K1[i].octave == 0;  // level1 > 0 -> continue (ORBmatcher.cc:615)
+    for (int i = tid; i < n1; i += KM_THREADS) s_m12[i] = K1[i].octave == 0;  // level1 > 0 -> continue (ORBmatcher.cc:615)
     if constexpr (BIG) __threadfence_block();
     __syncthreads();
     if (wave == 0) {  // in-place, in-order compaction (one wave: reads precede writes)
@@ -2350,7 +2351,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
     }
     KM_T(1);
     // rank F2 candidates by traversal key -> slot
-    for (int t = tid; t < n2c; t += 256) {
+    for (int t = tid; t < n2c; t += KM_THREADS) {
         const uint32_t k = s_key[t];
         int rank = 0;
         for (int u = 0; u < n2c; ++u) rank += s_key[u] < k;
@@ -2364,7 +2365,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
 #pragma unroll
         for (int w = 0; w < 8; ++w) s_d2[rank * 8 + w] = D2[(long long)i2 * 8 + w];
     }
-    for (int q = tid; q < n1c; q += 256) {
+    for (int q = tid; q < n1c; q += KM_THREADS) {
         const int i1 = s_q2i[q];
         const orb_keypoint_t kp = K1[i1];
         s_qx[q] = prev ? prev[((long long)p * cap + i1) * 2] : kp.x;
@@ -2372,7 +2373,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
     }
     if constexpr (BIG) __threadfence_block();
     __syncthreads();
-    for (int i = tid; i < n1; i += 256) {
+    for (int i = tid; i < n1; i += KM_THREADS) {
         s_m12[i] = -1;
         s_bslot[i] = -1;
     }
@@ -2389,9 +2390,10 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
     }
     __syncthreads();
     KM_T(2);
-    // ---- phase 1: per-query top-8 (dist, order) ----
-    for (int q0 = 0; q0 < n1c; q0 += 256) {
-        const int q = q0 + tid;
+    // ---- phase 1: per-query top-8 (dist, order), two lanes per query (candidates j of one
+    // parity each), their sorted lists merged on DPP ----
+    for (int q0 = 0; q0 < n1c; q0 += KM_THREADS / 2) {
+        const int q = q0 + (tid >> 1), sub = tid & 1;
         const bool act = q < n1c;
         float qx = 0.f, qy = 0.f;
         int minCX = 1, maxCX = 0, minCY = 1, maxCY = 0;
@@ -2413,7 +2415,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
         int cnt = 0;
         // the window's grid columns only (an empty column range gives j0 >= j1)
         const int j0 = s_col[min(minCX, 64)], j1 = s_col[max(maxCX + 1, 0)];
-        for (int j = j0; j < j1; ++j) {
+        for (int j = j0 + sub; j < j1; j += 2) {
             const int cell = s_cell[j];
             const int cx = cell / 48, cy = cell - cx * 48;
             if (cx < minCX || cx > maxCX || cy < minCY || cy > maxCY) continue;
@@ -2422,9 +2424,24 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
             topk_insert(top, ((uint32_t)dist << KB) | (uint32_t)j);
             ++cnt;
         }
-        if (act) {
+        // merge with the partner lane's list: the 8 smallest of two sorted lists are
+        // min(a[i], b[7-i]) (a bitonic sequence), sorted by a 3-stage bitonic merge
+        cnt += lane_xor1(cnt);
+        uint32_t m8[MATCH_TOPK];
 #pragma unroll
-            for (int k = 0; k < MATCH_TOPK; ++k) s_list[q * MATCH_TOPK + k] = top[k];
+        for (int k = 0; k < MATCH_TOPK; ++k) m8[k] = min(top[k], (uint32_t)lane_xor1((int)top[MATCH_TOPK - 1 - k]));
+#pragma unroll
+        for (int d = 4; d >= 1; d >>= 1)
+#pragma unroll
+            for (int k = 0; k < MATCH_TOPK; ++k)
+                if ((k & d) == 0) {
+                    const uint32_t lo = min(m8[k], m8[k + d]), hi = max(m8[k], m8[k + d]);
+                    m8[k] = lo;
+                    m8[k + d] = hi;
+                }
+        if (act && sub == 0) {
+#pragma unroll
+            for (int k = 0; k < MATCH_TOPK; ++k) s_list[q * MATCH_TOPK + k] = m8[k];
             s_lcnt[q] = cnt;
         }
     }
@@ -2541,7 +2558,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
         if (tid < 32) s_hist[tid] = 0;
         __syncthreads();
         // rotation bin of every accepted i1, the stolen ones included (ORBmatcher.cc:664-676)
-        for (int i = tid; i < n1; i += 256) {
+        for (int i = tid; i < n1; i += KM_THREADS) {
             const int sl = s_bslot[i];
             if (sl < 0) continue;
             float rot = K1[i].angle - s_a2[sl];
@@ -2585,14 +2602,14 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
         }
         __syncthreads();
         const int i1x = s_ind[0], i2x = s_ind[1], i3x = s_ind[2];
-        for (int i = tid; i < n1; i += 256) {
+        for (int i = tid; i < n1; i += KM_THREADS) {
             const int bn = s_bslot[i];
             if (bn >= 0 && bn != i1x && bn != i2x && bn != i3x) s_m12[i] = -1;
         }
         __syncthreads();
     }
     int nm = 0;
-    for (int i = tid; i < n1; i += 256) {
+    for (int i = tid; i < n1; i += KM_THREADS) {
         const int m = s_m12[i];
         A.m12out[(long long)p * cap + i] = m;
         if (m >= 0) {
@@ -2606,7 +2623,12 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
     nm = wave_total(nm);
     if (lane == 0) s_hist[wave] = nm;
     __syncthreads();
-    if (tid == 0) A.nmOut[p] = s_hist[0] + s_hist[1] + s_hist[2] + s_hist[3];
+    if (tid == 0) {
+        int t = 0;
+#pragma unroll
+        for (int w = 0; w < KM_THREADS / 64; ++w) t += s_hist[w];
+        A.nmOut[p] = t;
+    }
 #if KM_TIMING
     KM_T(5);
     if (tid == 0 && !BIG) {
@@ -2628,7 +2650,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
 // keypoints), its staged arrays in the pair's own slot of the global scratch `big` (null when
 // cap <= A.nmax: nothing can overflow).  The dynamic LDS covers both bodies' needs, so no
 // second launch and nothing per call beyond this kernel.
-__global__ void __launch_bounds__(256) k_match_init(MatchArgs A, uint8_t* __restrict__ big, int nmaxBig) {
+__global__ void __launch_bounds__(KM_THREADS) k_match_init(MatchArgs A, uint8_t* __restrict__ big, int nmaxBig) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int p = blockIdx.x;
     if (match_pair<false>(A, p, A.nmax, smem, nullptr) && big) {
@@ -3913,7 +3935,7 @@ int orb_search_for_initialization_batch_device(const orb_keypoint_t* d_kps, cons
     void* big = nullptr;
     if (cap > nmax)  // a pair may overflow the LDS capacity: its slot of the large-capacity scratch
         if (int r = match_big_scratch(st, match_big_slot_bytes(cap, nmaxBig) * (size_t)P, &big)) return r;
-    hipLaunchKernelGGL(k_match_init, dim3(P), dim3(256), lds, st, A, (uint8_t*)big, nmaxBig);
+    hipLaunchKernelGGL(k_match_init, dim3(P), dim3(KM_THREADS), lds, st, A, (uint8_t*)big, nmaxBig);
     HIP_TRY(hipGetLastError());
     return ORB_OK;
 }
