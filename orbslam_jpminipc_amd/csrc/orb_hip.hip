@@ -2196,7 +2196,10 @@ struct MatchGeom {
 //            descriptors / coordinates / top-8 lists live in the pair's global scratch slot
 //            (L2-resident); up to 8192 keypoints per frame.
 #define MATCH_TOPK 8
+#ifndef KM_THREADS
 #define KM_THREADS 512  // one workgroup (8 waves) per pair: at most a few pairs share a CU
+#endif
+#define KM_LPQ (KM_THREADS / 256)  // phase-1 lanes per query (2 or 4)
 #define MATCH_BIG_NMAX 8192
 #ifndef KM_TIMING  // 1: per-phase s_memrealtime sums of k_match_init's pairs (experiment builds only)
 #define KM_TIMING 0
@@ -2392,8 +2395,8 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
     KM_T(2);
     // ---- phase 1: per-query top-8 (dist, order), two lanes per query (candidates j of one
     // parity each), their sorted lists merged on DPP ----
-    for (int q0 = 0; q0 < n1c; q0 += KM_THREADS / 2) {
-        const int q = q0 + (tid >> 1), sub = tid & 1;
+    for (int q0 = 0; q0 < n1c; q0 += KM_THREADS / KM_LPQ) {
+        const int q = q0 + tid / KM_LPQ, sub = tid & (KM_LPQ - 1);
         const bool act = q < n1c;
         float qx = 0.f, qy = 0.f;
         int minCX = 1, maxCX = 0, minCY = 1, maxCY = 0;
@@ -2415,7 +2418,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
         int cnt = 0;
         // the window's grid columns only (an empty column range gives j0 >= j1)
         const int j0 = s_col[min(minCX, 64)], j1 = s_col[max(maxCX + 1, 0)];
-        for (int j = j0 + sub; j < j1; j += 2) {
+        for (int j = j0 + sub; j < j1; j += KM_LPQ) {
             const int cell = s_cell[j];
             const int cx = cell / 48, cy = cell - cx * 48;
             if (cx < minCX || cx > maxCX || cy < minCY || cy > maxCY) continue;
@@ -2424,21 +2427,32 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
             topk_insert(top, ((uint32_t)dist << KB) | (uint32_t)j);
             ++cnt;
         }
-        // merge with the partner lane's list: the 8 smallest of two sorted lists are
-        // min(a[i], b[7-i]) (a bitonic sequence), sorted by a 3-stage bitonic merge
-        cnt += lane_xor1(cnt);
+        // merge with the partner lanes' lists (DPP quad_perm xor 1, then xor 2): the 8 smallest
+        // of two sorted lists are min(a[i], b[7-i]) (a bitonic sequence), sorted by a 3-stage
+        // bitonic merge
         uint32_t m8[MATCH_TOPK];
 #pragma unroll
-        for (int k = 0; k < MATCH_TOPK; ++k) m8[k] = min(top[k], (uint32_t)lane_xor1((int)top[MATCH_TOPK - 1 - k]));
+        for (int k = 0; k < MATCH_TOPK; ++k) m8[k] = top[k];
+        auto merge_round = [&](auto ctlC) {
+            constexpr int ctl = decltype(ctlC)::value;
+            cnt += __builtin_amdgcn_mov_dpp(cnt, ctl, 0xF, 0xF, false);
+            uint32_t o[MATCH_TOPK];
 #pragma unroll
-        for (int d = 4; d >= 1; d >>= 1)
+            for (int k = 0; k < MATCH_TOPK; ++k) o[k] = (uint32_t)__builtin_amdgcn_mov_dpp((int)m8[MATCH_TOPK - 1 - k], ctl, 0xF, 0xF, false);
 #pragma unroll
-            for (int k = 0; k < MATCH_TOPK; ++k)
-                if ((k & d) == 0) {
-                    const uint32_t lo = min(m8[k], m8[k + d]), hi = max(m8[k], m8[k + d]);
-                    m8[k] = lo;
-                    m8[k + d] = hi;
-                }
+            for (int k = 0; k < MATCH_TOPK; ++k) m8[k] = min(m8[k], o[k]);
+#pragma unroll
+            for (int d = 4; d >= 1; d >>= 1)
+#pragma unroll
+                for (int k = 0; k < MATCH_TOPK; ++k)
+                    if ((k & d) == 0) {
+                        const uint32_t lo = min(m8[k], m8[k + d]), hi = max(m8[k], m8[k + d]);
+                        m8[k] = lo;
+                        m8[k + d] = hi;
+                    }
+        };
+        merge_round(std::integral_constant<int, 0xB1>{});
+        if constexpr (KM_LPQ == 4) merge_round(std::integral_constant<int, 0x4E>{});
         if (act && sub == 0) {
 #pragma unroll
             for (int k = 0; k < MATCH_TOPK; ++k) s_list[q * MATCH_TOPK + k] = m8[k];
