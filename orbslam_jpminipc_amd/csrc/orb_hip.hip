@@ -2464,10 +2464,12 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
     KM_T(3);
     // ---- phase 2: the sequential greedy pass (ORBmatcher.cc:611-680) on one wave ----
     // Speculated eight queries at a time (lane 8g + c: query q0 + g, candidate c of its top-8),
-    // exact: query q reads only the states of its first min(cnt, 8) slots, and an accepted query
-    // changes exactly one slot (its best).  So every query of the batch is decided from the
-    // batch-start state unless an earlier query of the batch accepted a slot in its top-8, or it
-    // needs the window rescan (a truncated top-8 with < 2 live candidates); the batch commits
+    // exact: query q's outcome is fixed by its best and second live candidates (the first two of
+    // its sorted top-8 whose vMatchedDistance exceeds their distance), and an accepted query
+    // changes exactly one slot (its best), lowering its vMatchedDistance.  So every query of the
+    // batch is decided from the batch-start state unless an earlier query of the batch accepted
+    // its best or second slot (a live slot can only die; a taken best is a steal), or it needs
+    // the window rescan (a truncated top-8 with < 2 live candidates); the batch commits
     // its queries before the first such one (their slots are distinct, their vnMatches21
     // predecessors precede the batch) and the next batch starts there.  A rescan query heading
     // a batch runs alone on the whole wave.
@@ -2500,7 +2502,11 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
             for (int g2 = 0; g2 < 7; ++g2) {
                 if (!((accM >> (8 * g2)) & 1ull)) continue;  // wave-uniform
                 const int bs = __builtin_amdgcn_readlane(bestSlot, 8 * g2);
-                hit = hit || (grp > g2 && cand < k && (int)(e & SLOT) == bs);
+                // query g's decision reads only its best and second live candidates (the
+                // rescan test included: both live means >= 2 live): another slot of its top-8
+                // that an earlier query takes cannot change it
+                hit = hit || (grp > g2 && ((best != 0xFFFFFFFFu && bestSlot == bs) ||
+                                           (sec != 0xFFFFFFFFu && (int)(sec & SLOT) == bs)));
             }
             const uint64_t stopM = __ballot(hit || (rescan && cand == 0));
             const int jstop = stopM ? (__ffsll((unsigned long long)stopM) - 1) >> 3 : 8;
