@@ -868,12 +868,13 @@ __device__ __forceinline__ uint32_t compass4(uint32_t c, uint32_t q0, uint32_t q
 // ---- FAST strength --------------------------------------------------------------------------
 // S(p) = 1 + cornerScore<16>(p) of cv::FAST: the largest t for which p is a corner is S - 1,
 // so p is a corner at threshold t <=> S > t; records carry S - 1 as the score.
-// Both sides in one packed register of two exact f16 integers: lane 0 carries the dark
-// contrast v - c, lane 1 the bright contrast c - v.  A byte b is the f16 1024 + b (bits
-// 0x6400 | b), so (1024 + v, 1024 + c) is one v_lshl_or and the pair of contrasts one
-// v_pk_add_f16 with swapped, negated operand halves; all values are integers in [-255, 255],
-// exact in f16.  Arcs of 9 as windows of 3 (two v_pk_minimum3_f16 per arc, gfx950), the
-// best arc by v_pk_maximum3_f16: ~75 VALU per pixel, half the i16 version's.  Cheap enough to
+// Both sides in one packed register of two exact f16 values: lane 0 carries the dark
+// contrast v - c, lane 1 the bright contrast c - v, as multiples of 2^-24 (a byte b loaded
+// into a VGPR is the f16 denormal b * 2^-24, so the pair is one v_pk_add_f16 of the two
+// loaded bytes, no packing; all values are integers in [-255, 255] times 2^-24, exact).  Arcs
+// of 9 as windows of 3 (two v_pk_minimum3_f16 per arc, gfx950), the best arc by
+// v_pk_maximum3_f16: ~45 VALU per pixel (round 2's 1024 + b normal encoding needed a shift and
+// an or per circle pixel before the add: ~75; the i16 version ~150).  Cheap enough to
 // run on every pre-filter survivor instead of a 9-arc test followed by a second gather for the
 // corners (k_fast's queue is LDS-latency bound).
 #ifndef FS_I16  // 1: the previous i16 arithmetic (experiments)
@@ -907,12 +908,16 @@ __device__ __forceinline__ int fast_strength_packed(const uint8_t* p, int TP) {
     }
     return max((int)best.x, (int)best.y);
 #else
-    const uint32_t V = 0x64006400u | v;
+    // a byte b read into a VGPR is the f16 denormal b * 2^-24: (v - c, c - v) is one v_pk_add_f16
+    // of the two loaded bytes with both lanes on the low halves and one side negated per lane
+    // (exact: differences of denormals are exact; f16 denormals are not flushed)
     f16x2_t d[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        const f16x2_t P = __builtin_bit_cast(f16x2_t, V | ((uint32_t)p[off[k]] << 16));  // (1024+v, 1024+c)
-        d[k] = P - __builtin_shufflevector(P, P, 1, 0);                                  // (v - c, c - v)
+        const uint32_t c = p[off[k]];
+        uint32_t r;
+        asm("v_pk_add_f16 %0, %1, %2 op_sel_hi:[0,0] neg_lo:[0,1] neg_hi:[1,0]" : "=v"(r) : "v"(v), "v"(c));
+        d[k] = __builtin_bit_cast(f16x2_t, r);
     }
     f16x2_t m3[16];
 #pragma unroll
@@ -925,7 +930,10 @@ __device__ __forceinline__ int fast_strength_packed(const uint8_t* p, int TP) {
         const f16x2_t c = k + 1 < 16 ? __builtin_elementwise_minimum(__builtin_elementwise_minimum(m3[k + 1], m3[(k + 4) & 15]), m3[(k + 7) & 15]) : a;
         best = __builtin_elementwise_maximum(__builtin_elementwise_maximum(best, a), c);
     }
-    return max((int)best.x, (int)best.y);
+    // back to integers: a positive denormal's bits are its value; a negative one (or -0) is a
+    // negative i16 (sign bit set), and S <= 0 is no corner at any threshold >= 0
+    const uint32_t bb = __builtin_bit_cast(uint32_t, best);
+    return max((int)(short)(bb & 0xFFFFu), (int)(short)(bb >> 16));
 #endif
 }
 
@@ -1683,6 +1691,9 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     };
     // (2) compass pre-filter over the flattened tile + ring, 64 dwords per wave and step
+#if KF_TIMING
+    unsigned long long kft2 = 0;
+#endif
     {
         int qn = 0;
         const int nF = (t.th + 2) * fw, iw = t.sp >> 2;
@@ -1711,7 +1722,9 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
             pq[v ? qn + __popcll(m & below) : FT_Q] = (uint16_t)(((uint32_t)f << 4) | mask);
             qn += __popcll(m);
         }
-        KF_T(2);
+#if KF_TIMING
+        kft2 = __builtin_amdgcn_s_memrealtime();
+#endif
         drain(qn);
         if (np) strength_pass(0, np);  // the remainder, < 64 pixels
     }

@@ -1,10 +1,12 @@
 """The FAST strength arithmetic of `fast_strength_packed` (orb_hip.hip): contrasts as exact f16
-integers (a byte b is the f16 1024 + b), arcs of 9 as three windows of 3 (the kernel's
-v_pk_minimum3_f16), the best arc by maximum.  Emulated here in numpy float16 (IEEE binary16,
-the same rounding as the hardware) and checked (1) to stay exact: every intermediate equals
-the integer value; (2) to give S = 1 + cornerScore of cv::FAST, against the oracle's FAST
-(ORBextractor.cc:602 `FAST(..., true)`) on 7x7 patches: a corner at threshold t
-iff S > t, response S - 1."""
+denormals (a byte b loaded into a register is the binary16 bit pattern b = b * 2^-24), arcs of
+9 as three windows of 3 (the kernel's v_pk_minimum3_f16), the best arc by maximum, and the
+result read back as the int16 view of its bits.  Emulated here in numpy float16 (IEEE
+binary16 with gradual underflow, the same as the hardware with f16 denormals enabled, which
+the kernels' code objects declare: .amdhsa_float_denorm_mode_16_64 3) and checked (1) to stay
+exact: every intermediate equals the integer value times 2^-24; (2) to give S = 1 + cornerScore
+of cv::FAST, against the oracle's FAST (ORBextractor.cc:602 `FAST(..., true)`) on
+7x7 patches: a corner at threshold t iff S > t, response S - 1."""
 import ctypes
 
 import numpy as np
@@ -23,15 +25,23 @@ def _arcs(d):
     return w9.max(axis=1), m3, w9
 
 
+def _den(b):
+    """bytes -> the binary16 values with those bit patterns (denormals b * 2^-24)"""
+    return b.astype(np.uint16).view(np.float16)
+
+
 def strength_f16(v, c):
-    V = (1024 + v.astype(np.int32)).astype(np.float16)[:, None]
-    C = (1024 + c.astype(np.int32)).astype(np.float16)
+    V = _den(v)[:, None]
+    C = _den(c)
     out, inter = [], []
     for d in (V - C, C - V):  # (v - c, c - v): the kernel's two f16 lanes
         best, m3, w9 = _arcs(d)
         out.append(best)
         inter += [d, m3, w9, best]
-    return np.maximum(out[0], out[1]), inter
+    # the kernel's read-back: int16 view of each lane's bits (negatives and -0 come out < 0),
+    # the larger of the two lanes
+    S = np.maximum(out[0].view(np.int16), out[1].view(np.int16)).astype(np.int32)
+    return S, inter
 
 
 def strength_int(v, c):
@@ -68,14 +78,16 @@ def test_f16_strength_is_exact():
     sf, inf = strength_f16(v, c)
     si, ini = strength_int(v, c)
     for a, b in zip(inf, ini):
-        assert np.array_equal(a.astype(np.int32), b), "an f16 intermediate is not the exact integer"
-    assert np.array_equal(sf.astype(np.int32), si)
+        assert np.array_equal((a.astype(np.float64) * 2.0 ** 24), b), "an f16 intermediate is not exact"
+    # S > 0 exactly; S <= 0 reads back <= 0 (no corner at any threshold >= 0)
+    assert np.array_equal(np.where(si > 0, sf, 0), np.where(si > 0, si, 0))
+    assert (sf[si <= 0] <= 0).all()
     assert si.min() >= -255 and si.max() <= 255
 
 
 def test_f16_strength_is_cornerscore_plus_one():
     v, c = _cases(3000, 2)
-    S = strength_f16(v, c)[0].astype(np.int32)
+    S = strength_f16(v, c)[0]
     rng = np.random.default_rng(3)
     L = lib()
     out = np.zeros(3 * 4, np.int32)
