@@ -744,6 +744,7 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
                     if (cc[j] & (1u << 27)) live |= 0xFFu << (8 * j);
                 }
                 const bool allSimd = simd == 0xFu;
+                const uint32_t hmask = allSimd ? 0xFFFFFFF0u : 0xFFFFFFFFu;  // (H >> 4) << 4 on all-SSE2 quads
                 // HResizeLinear of the source row at LDS address `ra`: H = S[sx] a0 + S[sx+1] a1
                 // (a1 == 0 where OpenCV reads S[sx] only: the byte after it is multiplied by 0; it
                 // lies in the ring row's slack or the next LDS row, never outside the allocation).
@@ -760,7 +761,7 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
                     for (int j = 0; j < 4; ++j) {
                         const uint32_t H = __builtin_amdgcn_udot2(__builtin_bit_cast(ps_u16x2, lo8[j] | (hi8[j] << 16)),
                                                                   __builtin_bit_cast(ps_u16x2, ap[j]), 0u, false);
-                        hh[j] = allSimd ? (H & 0xFFFFFFF0u) : H;
+                        hh[j] = H & hmask;
                     }
                 };
                 const int cx = 4 * q - EDGE;
