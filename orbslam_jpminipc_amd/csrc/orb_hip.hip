@@ -970,6 +970,7 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
             ((uint32_t*)Fl)[i] = 0u;
             ((uint32_t*)Sp)[i] = 0u;  // a pixel the compass rejects keeps strength 0
         }
+        for (int i = tid; i < dh; i += 256) rowc[i] = 0;
     }
     __syncthreads();
     // the strength plane (corner at t <=> S > t; the NMS below reads only S > t, so a pixel
@@ -994,7 +995,8 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
             if (lane < n) {
                 const int i = q[base + lane];
                 const int yy = dw > 1 ? (int)__umulhi((uint32_t)i, m) : i, xx = i - yy * dw;
-                Sp[yy * dwp + xx] = (uint8_t)max(fast_strength_packed(In + (yy + 3) * inW + xx + 3 + o, inW), 0);
+                const int S = fast_strength_packed(In + (yy + 3) * inW + xx + 3 + o, inW);
+                Sp[yy * dwp + xx] = (uint8_t)(S > t ? S : 0);  // only corners at t carry a strength
             }
         };
         // one strength call site (the last round flushes the queue's remainder)
@@ -1034,32 +1036,61 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
         }
     }
     __syncthreads();
-    // 3x3 NMS; each row's survivor count comes from the same ballots (no second pass)
-    const uint32_t* Flw = (const uint32_t*)Fl;
-    for (int yy = wave; yy < dh; yy += 4) {
-        int rc = 0;
-        for (int xx0 = 0; xx0 < dw; xx0 += 64) {
-            const int xx = xx0 + lane;
-            bool keep = false;
-            if (xx < dw) {
-                const int s0 = Sp[yy * dwp + xx];
-                if (s0 > t) {
-                    keep = true;
-#pragma unroll
-                    for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-                        for (int dx = -1; dx <= 1; ++dx) {
-                            if (dx == 0 && dy == 0) continue;
-                            const int nx = xx + dx, ny = yy + dy;
-                            const int n = (nx >= 0 && nx < dw && ny >= 0 && ny < dh) ? Sp[ny * dwp + nx] : 0;
-                            keep = keep && (s0 - 1 > (n > t ? n - 1 : 0));
-                        }
+    // 3x3 NMS on the corners only: Sp holds S where S > t and 0 elsewhere, so cv::FAST's strict
+    // test s0 - 1 > (n > t ? n - 1 : 0) reads the plane as is (out-of-cell neighbours 0).  Each
+    // wave scans its share of the plane's dwords, ballot-compacts the nonzero pixels into its
+    // queue (the strength pass is done with it) and runs the NMS one corner per lane, all nine
+    // reads issued together; a survivor sets its flag and counts into its row (LDS atomics)
+    {
+        uint32_t* q = (uint32_t*)(In + inW * (dh + 6)) + 4 + wave * (RR_Q + 8);
+        const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+        const uint32_t* Sp32 = (const uint32_t*)Sp;
+        const uint32_t mr = rw > 1 ? (uint32_t)((0x100000000ull + rw - 1) / (uint64_t)rw) : 0u;
+        auto nms = [&](int n) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            for (int k0 = 0; k0 < n; k0 += 64) {
+                if (k0 + lane < n) {
+                    const uint32_t code = q[k0 + lane];
+                    const int yy = (int)(code >> 16), xx = (int)(code & 0xFFFFu);
+                    const uint8_t* sp = Sp + yy * dwp + xx;
+                    const int s0 = sp[0];
+                    const bool xl = xx > 0, xr = xx + 1 < dw, yu = yy > 0, yd = yy + 1 < dh;
+                    const int n0 = (yu && xl) ? sp[-dwp - 1] : 0, n1 = yu ? sp[-dwp] : 0, n2 = (yu && xr) ? sp[-dwp + 1] : 0;
+                    const int n3 = xl ? sp[-1] : 0, n4 = xr ? sp[1] : 0;
+                    const int n5 = (yd && xl) ? sp[dwp - 1] : 0, n6 = yd ? sp[dwp] : 0, n7 = (yd && xr) ? sp[dwp + 1] : 0;
+                    const int m = max(max(max(n0, n1), max(n2, n3)), max(max(n4, n5), max(n6, n7)));
+                    if (s0 > m) {  // s0 > t: a stored strength
+                        Fl[yy * dwp + xx] = 1;
+                        atomicAdd(&rowc[yy], 1);
+                    }
                 }
             }
-            if (keep) Fl[yy * dwp + xx] = 1;
-            rc += __popcll(__ballot(keep));
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        };
+        int cn = 0;
+        for (int i0 = wave * 64; i0 < nw; i0 += 256) {  // wave-uniform
+            const int i = i0 + lane;
+            uint32_t w4 = 0u;
+            int yy = 0, wd = 0;
+            if (i < nw) {
+                yy = rw > 1 ? (int)__umulhi((uint32_t)i, mr) : i;
+                wd = i - yy * rw;
+                w4 = Sp32[i];
+            }
+            if (__ballot(w4 != 0u) == 0ull) continue;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const bool v = ((w4 >> (8 * j)) & 0xFFu) != 0u;
+                const uint64_t m = __ballot(v);
+                q[v ? cn + __popcll(m & below) : RR_Q] = ((uint32_t)yy << 16) | (uint32_t)(4 * wd + j);
+                cn += __popcll(m);
+            }
+            if (cn > RR_Q - 256) {
+                nms(cn);
+                cn = 0;
+            }
         }
-        if (lane == 0) rowc[yy] = rc;
+        if (cn) nms(cn);
     }
     __syncthreads();
     __shared__ int s_total;
@@ -1075,6 +1106,7 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
         if (lane == 0) s_total = carry;
     }
     __syncthreads();
+    const uint32_t* Flw = (const uint32_t*)Fl;
     for (int yy = wave; yy < dh; yy += 4) {
         int off = rowc[yy];
         const uint32_t ly = (uint32_t)(ry0 + yy) << 12;
