@@ -2543,17 +2543,12 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
                                 (float)bestDist < (float)second * nnratio;
             // first query the batch-start state cannot decide
             const uint64_t accM = __ballot(accept && cand == 0);  // bit 8g: group g accepts
-            bool hit = false;
-#pragma unroll
-            for (int g2 = 0; g2 < 7; ++g2) {
-                if (!((accM >> (8 * g2)) & 1ull)) continue;  // wave-uniform
-                const int bs = __builtin_amdgcn_readlane(bestSlot, 8 * g2);
-                // query g's decision reads only its best and second live candidates (the
-                // rescan test included: both live means >= 2 live): another slot of its top-8
-                // that an earlier query takes cannot change it
-                hit = hit || (grp > g2 && ((best != 0xFFFFFFFFu && bestSlot == bs) ||
-                                           (sec != 0xFFFFFFFFu && (int)(sec & SLOT) == bs)));
-            }
+            // lane 8g + c checks group c's accepted slot against query g's best and second
+            // (query g's decision reads only those two slots: the rescan test included, both
+            // live means >= 2 live), one ds_bpermute for the eight groups' slots
+            const int bsC = __shfl(bestSlot, 8 * cand, 64);
+            const bool hit = cand < grp && ((accM >> (8 * cand)) & 1ull) &&
+                             ((best != 0xFFFFFFFFu && bestSlot == bsC) || (sec != 0xFFFFFFFFu && (int)(sec & SLOT) == bsC));
             const uint64_t stopM = __ballot(hit || (rescan && cand == 0));
             const int jstop = stopM ? (__ffsll((unsigned long long)stopM) - 1) >> 3 : 8;
             if (accept && valid && e == best && grp < jstop) {
