@@ -2525,9 +2525,14 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
         while (q0 < n1c) {
             const int q = q0 + grp;
             const bool qin = q < n1c;
-            const int cnt = qin ? s_lcnt[q] : 0;
+            // the group's count, list entry and query index read together (one LDS round trip)
+            const int qc = min(q, n1c - 1);
+            const int cntR = s_lcnt[qc];
+            const uint32_t eR = s_list[qc * MATCH_TOPK + cand];
+            const int i1q = s_q2i[qc];
+            const int cnt = qin ? cntR : 0;
             const int k = min(cnt, MATCH_TOPK);
-            const uint32_t e = cand < k ? s_list[q * MATCH_TOPK + cand] : 0xFFFFFFFFu;
+            const uint32_t e = cand < k ? eR : 0xFFFFFFFFu;
             const uint2 st = cand < k ? s_st[e & SLOT] : make_uint2(0u, 0u);
             const bool valid = cand < k && (int)(st.x & 0xFFFFu) > (int)(e >> KB);
             // the group's best (smallest live key: the lists are sorted) and second, by 8-lane
@@ -2554,7 +2559,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
             if (accept && valid && e == best && grp < jstop) {
                 // by the best candidate's lane; distinct slots: these writes commute, and the
                 // next batch's reads follow them
-                const int i1 = s_q2i[q];
+                const int i1 = i1q;
                 const int old = (int)(st.x >> 16) - 1;  // vnMatches21[bestIdx2]
                 if (old >= 0) s_m12[old] = -1;
                 s_m12[i1] = (int)st.y;
