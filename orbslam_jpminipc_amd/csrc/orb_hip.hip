@@ -1107,8 +1107,10 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
     }
     __syncthreads();
     const uint32_t* Flw = (const uint32_t*)Fl;
+    const int totalK = s_total;
     for (int yy = wave; yy < dh; yy += 4) {
         int off = rowc[yy];
+        if ((yy + 1 < dh ? rowc[yy + 1] : totalK) == off) continue;  // no survivor in this row
         const uint32_t ly = (uint32_t)(ry0 + yy) << 12;
         for (int w0 = 0; w0 < rw; w0 += 64) {
             const int w = w0 + lane;
@@ -1126,9 +1128,8 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
             off += __builtin_amdgcn_readlane(incl, 63);
         }
     }
-    const int total = s_total;
     __syncthreads();  // smem is reused by the caller
-    return total;
+    return totalK;
 }
 
 // The FAST(7) re-runs of every (frame, level), at every batch size, before k_select<.., false>
