@@ -966,10 +966,11 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
         // all loads of a batch in flight before any LDS write (one round trip per 20 dwords
         // per thread, instead of one per row group)
         stage_rows_to_lds<256>((uint32_t*)In, nwr, src, pw, dh + 6, nwr, nwr, tid);
-        for (int i = tid; i < nw; i += 256) {
-            ((uint32_t*)Fl)[i] = 0u;
-            ((uint32_t*)Sp)[i] = 0u;  // a pixel the compass rejects keeps strength 0
-        }
+        // Sp and Fl (contiguous from the 16-B aligned smem) zeroed with 16-B stores: a pixel
+        // the compass rejects keeps strength 0
+        const int z16 = (2 * nw) >> 2;
+        for (int i = tid; i < z16; i += 256) ((uint4*)Sp)[i] = make_uint4(0u, 0u, 0u, 0u);
+        for (int i = 4 * z16 + tid; i < 2 * nw; i += 256) ((uint32_t*)Sp)[i] = 0u;
         for (int i = tid; i < dh; i += 256) rowc[i] = 0;
     }
     __syncthreads();
