@@ -1879,13 +1879,16 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
 //   * IC_Angle (ORBextractor.cc:124-151) on its raw 31x31 disc;
 //   * the descriptor image the reference reads after GaussianBlur(level ROI, 7x7, sigma 2)
 //     in place (ORBextractor.cc:760), only where rBRIEF samples it: the row pass of the
-//     fixed-point kernel (18, 34, 49, 55, 49, 34, 18) over the window's 44 rows x 40 columns
-//     (x-18 .. x+21) as u16 sums in LDS, rows interleaved in pairs; then per sample the column
-//     pass by four v_dot2 over row pairs, OpenCV's rounding for that column (SSE2 columns
+//     fixed-point kernel (18, 34, 49, 55, 49, 34, 18) over the window's rows on the matrix
+//     cores (three v_mfma_i32_16x16x64_i8 M-tiles x four N-tiles against a banded tap matrix),
+//     stored as u16 sums in LDS, rows interleaved in pairs; then per sample the column pass by
+//     four v_dot2 over row pairs, OpenCV's rounding for that column (SSE2 columns
 //     x < 4*floor(w/4) half-to-even, the scalar tail half-up), or the raw
 //     border byte where the sample lies outside the ROI (in-place ROI blur: the padding stays
 //     un-blurred).  Exact integers throughout (T <= 257 * 65535 < 2^24).
-// No workgroup barrier: a wave reads only what it wrote (LDS is in order per wave).
+// OD_WAVES keypoint slots per workgroup.  A wave's window and sums are its own (LDS is in order
+// per wave); the two workgroup barriers only hand the IC moments to wave 0, which computes the
+// slots' angle / sin / cos once, and hand those back.
 #ifndef OD_XCD  // 0: plain block order (experiments)
 #define OD_XCD 1
 #endif
