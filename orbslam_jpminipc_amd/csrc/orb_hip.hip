@@ -1621,6 +1621,10 @@ struct FastTile {
     uint32_t rcpU;      // ceil(2^32 / (sp / 16)): staged unit -> row
 };
 
+#ifndef KF_XCD
+#define KF_XCD 0  // 1: XCD-aware workgroup order; measured slower (0.646 vs 0.574 ms c3, 0.913
+                  // vs 0.832 c4, 1.627 vs 1.557 720p): the halo re-reads are not what binds
+#endif
 #ifndef KF_WAVES
 #define KF_WAVES 0  // > 0: waves per SIMD the register allocation targets
 #endif
@@ -1639,8 +1643,20 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
     __shared__ uint16_t s_q[4][FT_Q + 2];
     __shared__ uint16_t s_px[4][FT_CQ + 2];  // a chunk's pixels, compacted in place to its corners
     KF_T(0);
+#if KF_XCD
+    // XCD-aware order: workgroup i runs on XCD i % 8, so give each XCD a contiguous run of
+    // (frame, tile) ids — consecutive tiles are vertically adjacent in one column strip, and
+    // their shared halo rows then hit in that XCD's L2
+    int bid = blockIdx.y * gridDim.x + blockIdx.x;
+    const int full = (gridDim.x * gridDim.y) & ~7;
+    if (bid < full) bid = (bid & 7) * (full >> 3) + (bid >> 3);
+    const int b = (int)((uint32_t)bid / gridDim.x);
+    FastTile t = tiles[bid - b * (int)gridDim.x];
+#else
     FastTile t = tiles[blockIdx.x];
-    const int b = blockIdx.y, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int b = blockIdx.y;
+#endif
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     // the level's geometry and the tile in SGPRs for the whole kernel (read through a reference
     // into the kernarg block, the compiler re-issued dependent s_loads inside the loops); the
     // empty asm makes the copies opaque, so they cannot be rematerialised
