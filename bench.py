@@ -33,9 +33,14 @@ Also reported:
                 host frame through orb_extract, one frame pair through the host
                 SearchForInitialization, one device frame through orb_extract_batch_device; the
                 single-thread CPU oracle beside each (rank 0, N = 1)
+  host_fed      the same step fed from pinned host memory and returned to it (the operator()
+                boundary: ORBextractor.h:43-45), H2D / compute / D2H overlapped on three streams;
+                frames/s with the PCIe GB/s achieved each way and the link's measured ceiling
+                (rank 0, N = 1; never `value`)
   cpu_baseline  the CPU oracle (C++ restatement, oracle/) on the host cores, rank 0, N = 1, on a
                 bounded sample of the same frames: extract-only and extract+match frames/s on all
-                threads, single-thread ms/frame, CPU model
+                threads and on the cgroup quota's thread count (value = the better of the two,
+                with its thread count), single-thread ms/frame, CPU model
 --overlap 1 / 2 are measured-slower stream-overlap experiments; the default (0)
 is the serial step.  --dry-run runs the launcher and rank plumbing on CPU (gloo, the oracle as
 the per-rank workload) for the multi-process tests.
@@ -56,6 +61,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md §Chip-level parameters)
+N_CU, CLOCK_HZ = 256, 2.4e9
+SALU_PEAK = N_CU * CLOCK_HZ  # SALU instructions / s: one scalar unit per CU, one issue per cycle
+LDS_PEAK = N_CU * CLOCK_HZ   # LDS pipe cycles / s: one per CU per cycle
 METRIC = "frames/sec ORB extract+match, 640x480 8-level 1000 kp; HBM GB/s vs peak"
 
 WORKLOADS = {
@@ -363,6 +371,104 @@ def latency_b1(orb, W, H, NF, device, frames, reps=100):
     }
 
 
+def host_fed(ext, matcher, frames_h, f1, f2, W, H, steps, warmup):
+    """The step fed from host memory, as a caller of ORBextractor::operator() sees it
+    (ORBextractor.h:43-45: a host cv::Mat in, host keypoints / descriptors out; Frame.cc:60,
+    Tracking.cc:215-217): every step's B frames start in pinned host memory and its keypoint
+    records, descriptors, counts and SearchForInitialization results end in pinned host memory.
+    Three streams, double-buffered device and host buffers: H2D of batch t+1 and D2H of batch
+    t-1 overlap the extraction + matching of batch t (event-ordered, so a buffer is rewritten
+    only after its last reader).  Returns frames/s with the achieved PCIe rate each way and the
+    link's measured one-way ceiling (one large pinned copy each way, alone)."""
+    import torch
+
+    B = frames_h.shape[0]
+    cap = ext.max_keypoints
+    P = int(f1.numel())
+    h_in = torch.from_numpy(frames_h).pin_memory()
+    d_in = [torch.empty_like(h_in, device="cuda") for _ in range(2)]
+    d_out = [(torch.empty((B, cap, 28), dtype=torch.uint8, device="cuda"),
+              torch.empty((B, cap, 32), dtype=torch.uint8, device="cuda"),
+              torch.empty((B,), dtype=torch.int32, device="cuda")) for _ in range(2)]
+    d_m = [None, None]
+    h_out = [(torch.empty((B, cap, 28), dtype=torch.uint8).pin_memory(),
+              torch.empty((B, cap, 32), dtype=torch.uint8).pin_memory(),
+              torch.empty((B,), dtype=torch.int32).pin_memory(),
+              torch.empty((P, cap), dtype=torch.int32).pin_memory(),
+              torch.empty((P,), dtype=torch.int32).pin_memory()) for _ in range(2)]
+    s_h2d, s_comp, s_d2h = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+    ev_h2d = [torch.cuda.Event() for _ in range(2)]
+    ev_comp = [torch.cuda.Event() for _ in range(2)]
+    ev_d2h = [torch.cuda.Event() for _ in range(2)]
+    torch.cuda.synchronize()
+
+    def issue(t):
+        i = t % 2
+        with torch.cuda.stream(s_h2d):
+            if t >= 2:
+                s_h2d.wait_event(ev_comp[i])  # extraction t-2 has read d_in[i]
+            d_in[i].copy_(h_in, non_blocking=True)
+            ev_h2d[i].record(s_h2d)
+        with torch.cuda.stream(s_comp):
+            s_comp.wait_event(ev_h2d[i])
+            if t >= 2:
+                s_comp.wait_event(ev_d2h[i])  # D2H t-2 has read d_out[i]
+            kps, desc, cnt = d_out[i]
+            ext.extract_batch_device(d_in[i], kps, desc, cnt, stream=s_comp)
+            d_m[i] = matcher.search_for_initialization_batch_device(kps, desc, cnt, f1, f2, W, H, 100,
+                                                                    stream=s_comp)
+            ev_comp[i].record(s_comp)
+        with torch.cuda.stream(s_d2h):
+            s_d2h.wait_event(ev_comp[i])
+            hk, hd, hc, hm, hn = h_out[i]
+            hk.copy_(d_out[i][0], non_blocking=True)
+            hd.copy_(d_out[i][1], non_blocking=True)
+            hc.copy_(d_out[i][2], non_blocking=True)
+            hm.copy_(d_m[i][0], non_blocking=True)
+            hn.copy_(d_m[i][1], non_blocking=True)
+            ev_d2h[i].record(s_d2h)
+
+    for t in range(warmup):
+        issue(t)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for t in range(steps):
+        issue(t)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    in_bytes = h_in.numel()
+    out_bytes = sum(x.numel() * x.element_size() for x in h_out[0])
+
+    def one_way(src, dst, reps=5):
+        dst.copy_(src, non_blocking=True)
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        for _ in range(reps):
+            dst.copy_(src, non_blocking=True)
+        torch.cuda.synchronize()
+        return src.numel() * src.element_size() * reps / (time.perf_counter() - a) / 1e9
+
+    h2d_peak = one_way(h_in, d_in[0])
+    d2h_peak = one_way(d_in[0], h_in)
+    fps = B * steps / dt
+    return {
+        "value": fps,
+        "unit": "frames/s",
+        "ms_per_step": dt / steps * 1e3,
+        "steps": steps,
+        "h2d_bytes_per_step": in_bytes,
+        "d2h_bytes_per_step": out_bytes,
+        "h2d_GBps": in_bytes * steps / dt / 1e9,
+        "d2h_GBps": out_bytes * steps / dt / 1e9,
+        "h2d_link_GBps_measured": h2d_peak,
+        "d2h_link_GBps_measured": d2h_peak,
+        "input_bound_fps": h2d_peak * 1e9 / (in_bytes / B),
+        "note": f"{B} frames per step from pinned host memory; outputs (keypoint records, descriptors, counts, "
+                f"vnMatches12 of {P} pairs, nmatches) to pinned host memory at full capacity ({cap} slots per frame); "
+                "three streams, double-buffered; link ceilings: one pinned copy of the step's frames each way, alone",
+    }
+
+
 def run_rank(args):
     import torch
 
@@ -561,15 +667,27 @@ def run_rank(args):
     valu_insts = pmc.get("SQ_INSTS_VALU")
     # VALU issue ceiling: each SIMD issues one wave64 VALU instruction per 2 cycles
     # (MI355X_MICROARCH.md), 4 SIMDs x 256 CUs at 2.4 GHz
-    valu_peak = 256 * 4 / 2 * 2.4e9
+    valu_peak = N_CU * 4 / 2 * CLOCK_HZ
     # the roof that actually binds the dominant kernel: the larger of its VALU-issue fraction
     # and its PMC-measured HBM fraction (the algorithmic-bytes fraction below is the contract's
     # HBM roofline figure; it is not what limits these integer kernels)
     roofs = {}
+    launch_s = ds["ms_per_launch"] * 1e-3
     if valu_insts:
-        roofs["valu_issue"] = valu_insts / (ds["ms_per_launch"] * 1e-3) / valu_peak
+        roofs["valu_issue"] = valu_insts / launch_s / valu_peak
+    salu_insts = pmc.get("SQ_INSTS_SALU")
+    if salu_insts:
+        # one scalar unit per CU issuing one SALU instruction per cycle (MI355X_MICROARCH.md: 4
+        # SIMDs + 1 scalar unit per CU), shared by all the CU's waves
+        roofs["salu_issue"] = salu_insts / launch_s / SALU_PEAK
+    lds_insts, lds_conf = pmc.get("SQ_INSTS_LDS"), pmc.get("SQ_LDS_BANK_CONFLICT")
+    if lds_insts:
+        # the CU's LDS pipe: at least one cycle per wave64 LDS instruction (256 B/clk/CU, a
+        # dword per lane) plus every bank-conflict cycle the SQ counted (a lower bound on LDS
+        # busy time: b64 / b128 accesses take 2 / 4 cycles)
+        roofs["lds_issue"] = (lds_insts + (lds_conf or 0)) / launch_s / LDS_PEAK
     if traffic:
-        roofs["hbm_measured_traffic"] = traffic / (ds["ms_per_launch"] * 1e-3) / 1e9 / HBM_PEAK_GBS
+        roofs["hbm_measured_traffic"] = traffic / launch_s / 1e9 / HBM_PEAK_GBS
     binding = max(roofs, key=roofs.get) if roofs else None
     label = wl["label"] if not custom else f"custom {W}x{H}, ORBextractor({NF},1.2,8,FAST,20) + SearchForInitialization"
     result = {
@@ -612,7 +730,9 @@ def run_rank(args):
             "algorithmic_bytes_per_launch": ds["bytes_per_launch"],
             "algorithmic_bytes_basis": "SURVEY.md §8d, this stage's terms only (bench.stage_bytes)",
             "valu_insts_per_launch": valu_insts,
-            "valu_issue_frac": (valu_insts / (ds["ms_per_launch"] * 1e-3) / valu_peak) if valu_insts else None,
+            "valu_issue_frac": roofs.get("valu_issue"),
+            "salu_issue_frac": roofs.get("salu_issue"),
+            "lds_issue_frac": roofs.get("lds_issue"),
             # the other issue ports of the same PMC pass: SALU (one per CU per cycle) and the LDS
             # instructions with their bank-conflict cycles
             "salu_insts_per_launch": pmc.get("SQ_INSTS_SALU"),
@@ -623,7 +743,10 @@ def run_rank(args):
             "roofs": roofs,
             "bound_note": "bound/frac price the kernel against the HBM roofline with SURVEY §8d algorithmic "
                           "bytes (the contract's figure); `binding` names the roof that limits it, from the "
-                          "same PMC pass",
+                          "same PMC pass: valu_issue = SQ_INSTS_VALU / (1024 SIMDs x 1 per 2 cycles), "
+                          "salu_issue = SQ_INSTS_SALU / (256 CUs x 1 per cycle), lds_issue = (SQ_INSTS_LDS "
+                          "+ SQ_LDS_BANK_CONFLICT) / (256 CUs x 1 per cycle), hbm_measured_traffic = PMC "
+                          "bytes / 8 TB/s; all at 2.4 GHz over the event-timed launch",
         },
         "pipeline": {
             "algorithmic_bytes_per_step": b_ext + b_match,
@@ -637,6 +760,10 @@ def run_rank(args):
     if args.overlap:
         result["serial_step"] = {"value": frames_job * args.steps / serial_tmax,
                                  "ms_per_step": serial_tmax / args.steps * 1e3}
+    if rank == 0 and world == 1 and args.host_fed:
+        hf = host_fed(ext, matcher, frames, f1, f2, W, H, max(4, args.steps // 2), 2)
+        hf["vs_device_resident"] = hf["value"] / value
+        result["host_fed"] = hf
     if rank == 0 and world == 1 and args.latency:
         result["latency_b1"] = latency_b1(orb, W, H, NF, local, frames[:2])
     if rank == 0 and world == 1 and args.cpu_frames > 0:
@@ -648,14 +775,22 @@ def run_rank(args):
         quota = hc["cgroup_cpu_quota"]
         cb = cpu_baseline(cpu_frames, NF, threads, W, H, int(quota) if quota and quota >= 1 else None)
         pcores = physical_cores()
+        # value = the best measured CPU rate, with the thread count it ran at (the cgroup quota
+        # often makes the quota-sized run faster than one thread per affinity CPU)
+        best_fps, best_threads = cb["extract_match_fps"], threads
+        if cb.get("quota_threads_extract_match_fps", 0) > best_fps:
+            best_fps, best_threads = cb["quota_threads_extract_match_fps"], cb["quota_threads"]
         result["cpu_baseline"] = {
-            "value": cb["extract_match_fps"],
+            "value": best_fps,
             "unit": "frames/s",
-            "cores": threads,
+            "cores": best_threads,
+            "value_note": "the best measured CPU rate (extract + SearchForInitialization) with the threads it ran on; "
+                          "the affinity-set run, the quota-sized run and the all-physical-core estimate are beside it",
             "kind": "port",
             "sample": f"{ncpu} frames of stream 0, extract + {ncpu - 1} consecutive-pair SearchForInitialization "
                       f"(C++ restatement oracle, -O3 -march=native, scalar: not OpenCV's SSE2 build)",
             "extract_fps": cb["extract_fps"],
+            "affinity_threads": threads,
             "extract_match_fps": cb["extract_match_fps"],
             "single_thread_ms_per_frame_extract": cb["single_thread_ms_per_frame_extract"],
             "single_thread_ms_per_frame_extract_match": cb["single_thread_ms_per_frame_extract_match"],
@@ -680,6 +815,9 @@ def run_rank(args):
             result["cpu_baseline"]["machine_physical_cores"] = pcores
             result["cpu_baseline"]["estimate_all_physical_cores_fps"] = (
                 pcores * 1e3 / cb["single_thread_ms_per_frame_extract_match"])
+            result["cpu_baseline"]["gpu_over_estimate_all_physical_cores"] = value / (
+                pcores * 1e3 / cb["single_thread_ms_per_frame_extract_match"])
+        result["cpu_baseline"]["gpu_over_value"] = value / best_fps
     if rank == 0:
         print(json.dumps(result))
     replicas.shutdown(info)
@@ -704,6 +842,8 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=1536,
                     help="CPU-baseline sample size (0 = skip; at least 4 frames per thread)")
     ap.add_argument("--latency", type=int, default=1, help="1: measure latency_b1 (rank 0, N = 1)")
+    ap.add_argument("--host-fed", type=int, default=1,
+                    help="1: measure the host-fed step (pinned host frames in, host results out; rank 0, N = 1)")
     ap.add_argument("--overlap", type=int, default=0,
                     help="0 (default): serial step; 1 / 2: stream-overlap experiments, measured slower")
     ap.add_argument("--survey-steps", type=int, default=5, help="untimed steps with every stage bracketed")

@@ -148,6 +148,11 @@ int orb_search_for_initialization_batch_device(const orb_keypoint_t* d_kps, cons
                                                const int32_t* d_pair_f2, orb_frame_bounds_t bounds, float nnratio,
                                                int check_ori, int window, float* d_prev_xy, int32_t* d_matches12,
                                                int32_t* d_nmatches, void* stream);
+/* Release the large-capacity scratch kept for `stream` on the current device (freed in stream
+ * order, after the launches already queued on it).  Call before destroying a stream that ran
+ * orb_search_for_initialization_batch_device; a later call on the stream re-creates it.  No
+ * reference counterpart (resource hook of the batched entry point). */
+int orb_match_release_stream_scratch(void* stream);
 
 /* ---- the rest of the ORBmatcher family (GPU: csrc/orb_match.hip) ------------------- */
 /* All entry points below take HOST buffers, run on the device of `device`, and are

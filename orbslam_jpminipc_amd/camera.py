@@ -60,6 +60,22 @@ def compute_image_bounds(cols: int, rows: int, K, distCoef, device: int = -1) ->
     return b
 
 
+_BOUNDS = {}
+
+
+def image_bounds(cols: int, rows: int, K, distCoef) -> FrameBounds:
+    """The bounds Frame keeps: the reference computes them once, on the first frame, into
+    static members (Frame.cc:73-86, mbInitialComputations) and every later frame of the same
+    camera reuses them; here they are kept per (image size, K, distCoef), so only a new camera
+    or image size costs a device round trip.  Returns a copy (callers may not mutate the cache)."""
+    k4, d4 = camera_k4(K), dist4(distCoef)
+    key = (int(cols), int(rows), k4.tobytes(), d4.tobytes())
+    b = _BOUNDS.get(key)
+    if b is None:
+        b = _BOUNDS[key] = compute_image_bounds(cols, rows, k4, d4)
+    return FrameBounds(b.min_x, b.max_x, b.min_y, b.max_y)
+
+
 def undistort_keypoints_batch_device(d_kps, d_counts, K, distCoef, d_kps_un=None, stream=None):
     """orb_undistort_keypoints_batch_device on extractor output ((B, cap, 28) uint8 device
     tensor + (B,) int32 counts); returns d_kps_un (same shape), enqueued on `stream`."""

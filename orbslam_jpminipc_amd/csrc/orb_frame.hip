@@ -62,9 +62,10 @@ __device__ __forceinline__ void undistort_pt(const Camera& c, float xin, float y
     *yo = (float)(yy * ww);
 }
 
-__global__ void __launch_bounds__(256) k_undistort(const orb_keypoint_t* __restrict__ kps,
-                                                   const int32_t* __restrict__ counts, int cap, int B, Camera cam,
-                                                   orb_keypoint_t* __restrict__ out) {
+// kps and out may alias (the ABI allows d_kps_un == d_kps): no __restrict__ on them; each thread
+// reads its record before writing the same slot.
+__global__ void __launch_bounds__(256) k_undistort(const orb_keypoint_t* kps, const int32_t* __restrict__ counts,
+                                                   int cap, int B, Camera cam, orb_keypoint_t* out) {
     const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
     if (i >= (long long)B * cap) return;
     const int b = (int)(i / cap), k = (int)(i - (long long)b * cap);

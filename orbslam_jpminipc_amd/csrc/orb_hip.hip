@@ -3981,12 +3981,14 @@ static size_t match_big_lds_bytes(int cap, int nmax) { return (size_t)nmax * 8 +
 // (device, stream) so launches on one stream reuse it in stream order and concurrent streams
 // never share one.  Grown by a stream-ordered free + allocation on that stream; steady state:
 // no allocator call.  Only the slots of pairs that overflow the LDS capacity are ever touched.
+// The caller holds g_bigMu from the lookup until its launch is enqueued: two host threads
+// sharing one stream (e.g. the null stream) then cannot interleave a grow (whose free is
+// stream-ordered after the other thread's launch) between the other's lookup and launch.
 static std::mutex g_bigMu;
 static std::vector<std::pair<std::pair<int, hipStream_t>, std::pair<void*, size_t>>> g_big;
-static int match_big_scratch(hipStream_t st, size_t bytes, void** out) {
+static int match_big_scratch_locked(hipStream_t st, size_t bytes, void** out) {
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));
-    std::lock_guard<std::mutex> lk(g_bigMu);
     for (auto& e : g_big)
         if (e.first.first == dev && e.first.second == st) {
             if (e.second.second < bytes) {
@@ -4002,6 +4004,20 @@ static int match_big_scratch(hipStream_t st, size_t bytes, void** out) {
     HIP_TRY(hipMallocAsync(&p, bytes, st));
     g_big.push_back({{dev, st}, {p, bytes}});
     *out = p;
+    return ORB_OK;
+}
+
+int orb_match_release_stream_scratch(void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(g_bigMu);
+    for (size_t i = 0; i < g_big.size(); ++i)
+        if (g_big[i].first.first == dev && g_big[i].first.second == st) {
+            HIP_TRY(hipFreeAsync(g_big[i].second.first, st));  // after the stream's queued launches
+            g_big.erase(g_big.begin() + (long)i);
+            return ORB_OK;
+        }
     return ORB_OK;
 }
 
@@ -4043,8 +4059,11 @@ int orb_search_for_initialization_batch_device(const orb_keypoint_t* d_kps, cons
                 d_prev_xy, d_matches12, d_nmatches, P};
     hipStream_t st = (hipStream_t)stream;
     void* big = nullptr;
-    if (cap > nmax)  // a pair may overflow the LDS capacity: its slot of the large-capacity scratch
-        if (int r = match_big_scratch(st, match_big_slot_bytes(cap, nmaxBig) * (size_t)P, &big)) return r;
+    std::unique_lock<std::mutex> lk(g_bigMu, std::defer_lock);
+    if (cap > nmax) {  // a pair may overflow the LDS capacity: its slot of the large-capacity scratch
+        lk.lock();     // held until the launch that uses it is enqueued
+        if (int r = match_big_scratch_locked(st, match_big_slot_bytes(cap, nmaxBig) * (size_t)P, &big)) return r;
+    }
     hipLaunchKernelGGL(k_match_init, dim3(P), dim3(KM_THREADS), lds, st, A, (uint8_t*)big, nmaxBig);
     HIP_TRY(hipGetLastError());
     return ORB_OK;

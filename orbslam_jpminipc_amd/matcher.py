@@ -37,7 +37,7 @@ class Frame:
 
             if self.N:
                 self.mvKeysUn = camera.undistort_keypoints(self.mvKeys, K, distCoef)
-            b = camera.compute_image_bounds(width, height, K, distCoef)
+            b = camera.image_bounds(width, height, K, distCoef)  # once per camera (Frame.cc:73-86)
             self.mnMinX, self.mnMaxX, self.mnMinY, self.mnMaxY = b.min_x, b.max_x, b.min_y, b.max_y
 
     @classmethod

@@ -47,6 +47,25 @@ class FrontEndPipeline:
             ptr(d_desc), ptr(d_counts), FrameBounds(0, int(w), 0, int(h)), float(nnratio), int(bool(checkOri)),
             int(window), ptr(d_matches12), ptr(d_nmatches), ctypes.c_void_p(s.cuda_stream)))
 
+    def run_undistorted(self, d_imgs, K, distCoef, d_kps, d_kps_un, d_desc, d_counts, d_matches12, d_nmatches,
+                        nnratio=0.9, checkOri=True, window=100, stream=None):
+        """The same step for a calibrated camera with distortion (Frame::Frame's
+        UndistortKeyPoints, Frame.cc:69): keypoints are undistorted into d_kps_un between
+        extraction and matching, and the pairs are matched on mvKeysUn inside the camera's
+        ComputeImageBounds (Frame.cc:321-349).  k1 == 0 copies the records (Frame.cc:291-295)."""
+        import torch
+
+        from . import camera
+
+        B, h, w = d_imgs.shape
+        k4, d4 = camera.camera_k4(K), camera.dist4(distCoef)
+        b = camera.image_bounds(int(w), int(h), k4, d4)
+        s = stream if stream is not None else torch.cuda.current_stream(d_imgs.device)
+        check(self._lib.orb_pipeline_extract_undistort_and_match(
+            self._h, int(B), ptr(d_imgs), int(w), int(h), int(d_imgs.stride(1)), int(d_imgs.stride(0)), ptr(k4),
+            ptr(d4), ptr(d_kps), ptr(d_kps_un), ptr(d_desc), ptr(d_counts), b, float(nnratio), int(bool(checkOri)),
+            int(window), ptr(d_matches12), ptr(d_nmatches), ctypes.c_void_p(s.cuda_stream)))
+
     def profile_enable(self, enable: bool = True) -> None:
         check(self._lib.orb_pipeline_profile_enable(self._h, int(enable)))
 

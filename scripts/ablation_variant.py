@@ -28,8 +28,10 @@ units = [tmp / "csrc" / u for u in ("orb_hip.hip", "orb_match.hip", "orb_voc.hip
                                     "orb_pipeline.hip", "orb_persist.hip", "orb_frame.hip")]
 out = ROOT / "build" / "variants" / f"{name}.so"
 out.parent.mkdir(parents=True, exist_ok=True)
-flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
-         "-fno-gpu-flush-denormals-to-zero", "-fhip-fp32-correctly-rounded-divide-sqrt", "-mllvm", "-amdgpu-mfma-vgpr-form=1"]
+sys.path.insert(0, str(ROOT))
+from __graft_entry__ import hipcc_flags  # noqa: E402  (the library's flags, optional ones probed)
+
+flags = hipcc_flags()
 r = subprocess.run(["/opt/rocm/bin/hipcc", *flags, "-o", str(out), *map(str, units)], capture_output=True, text=True)
 shutil.rmtree(tmp)
 if r.returncode:

@@ -7,7 +7,7 @@ cd "$(dirname "$0")/.."
 NAME=$1; REV=${2:-HEAD}
 T=$(mktemp -d /tmp/orbrev_XXXX)
 git archive "$REV" orbslam_jpminipc_amd/csrc include | tar -x -C "$T"
-F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -fno-gpu-flush-denormals-to-zero -fhip-fp32-correctly-rounded-divide-sqrt -mllvm -amdgpu-mfma-vgpr-form=1"
+F="$(python3 __graft_entry__.py flags)"  # the library's own flags (optional ones probed)
 mkdir -p build/variants
 C=$T/orbslam_jpminipc_amd/csrc
 /opt/rocm/bin/hipcc $F -o build/variants/$NAME.so $C/orb_hip.hip $C/orb_match.hip $C/orb_voc.hip $C/orb_mappoint.hip $C/orb_pipeline.hip $C/orb_persist.hip $C/orb_frame.hip 2> build/variants/$NAME.log

@@ -4,7 +4,7 @@
 set -e
 cd "$(dirname "$0")/.."
 NAME=$1; shift
-F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -fno-gpu-flush-denormals-to-zero -fhip-fp32-correctly-rounded-divide-sqrt -mllvm -amdgpu-mfma-vgpr-form=1"
+F="$(python3 __graft_entry__.py flags)"  # the library's own flags (optional ones probed)
 S="orbslam_jpminipc_amd/csrc/orb_hip.hip orbslam_jpminipc_amd/csrc/orb_match.hip orbslam_jpminipc_amd/csrc/orb_voc.hip orbslam_jpminipc_amd/csrc/orb_mappoint.hip orbslam_jpminipc_amd/csrc/orb_pipeline.hip orbslam_jpminipc_amd/csrc/orb_persist.hip orbslam_jpminipc_amd/csrc/orb_frame.hip"
 mkdir -p build/variants
 /opt/rocm/bin/hipcc $F "$@" -o build/variants/$NAME.so $S 2> build/variants/$NAME.log

@@ -109,19 +109,64 @@ def test_bench_batch_c4_full_parity():
     _check_batch(frames, 2000, *_device_extract_and_match(frames, 2000, pairs), pairs=pairs)
 
 
+def _check_sampled(frames, nf, per, kps, desc, cnt, m12, nm, pairs, every=16):
+    """_check_batch on a sample of a stream batch: within each stream of `per` frames the pairs
+    (t, t+1) with t % every == 0 plus the stream's last pair, and every frame those pairs touch
+    (so each stream's first and last frame are always in).  The device ran the whole batch;
+    only the oracle side is sampled."""
+    B, H, W = frames.shape
+    sel_pairs = [p for p, (a, _) in enumerate(pairs) if (a % per) % every == 0 or (a % per) == per - 2]
+    sel_frames = sorted({f for p in sel_pairs for f in pairs[p]})
+    pos = {f: i for i, f in enumerate(sel_frames)}
+    ref = _oracle_extract_all(frames[sel_frames], nf)
+    for f in sel_frames:
+        ko, do = ref[pos[f]]
+        assert cnt[f] == len(ko), f
+        assert kps[f, : cnt[f]].tobytes() == ko.tobytes(), f"frame {f} keypoints"
+        assert desc[f, : cnt[f]].tobytes() == do.tobytes(), f"frame {f} descriptors"
+    for p in sel_pairs:
+        a, b = pairs[p]
+        k1, d1 = ref[pos[a]]
+        k2, d2 = ref[pos[b]]
+        prev = np.ascontiguousarray(np.stack([k1["x"], k1["y"]], 1).astype(np.float32))
+        no, m12o = search_for_initialization(k1, d1, k2, d2, W, H, prev, 0.9, True, 100)
+        assert nm[p] == no, p
+        assert np.array_equal(m12[p, : cnt[a]], m12o), p
+    return len(sel_frames), len(sel_pairs)
+
+
 def test_bench_batch_c5_full_parity():
-    """bench.py --workload c5's timed batch at N = 1: 8 independent 1280x720 streams x 128
-    frames (B = 1024), ORBextractor(2500, 1.2, 8), the 8 x 127 within-stream pairs: every frame
-    and every pair bit-exact."""
+    """8 independent 1280x720 streams x 128 frames (B = 1024), ORBextractor(2500, 1.2, 8), the
+    8 x 127 within-stream pairs: every frame and every pair bit-exact (a smaller batch than
+    bench.py's default c5 step; that one is test_bench_batch_c5_default_step_sampled)."""
     frames, pairs = _bench_stream_batch(1280, 720, range(8), 128)
     _check_batch(frames, 2500, *_device_extract_and_match(frames, 2500, pairs), pairs=pairs)
 
 
+def test_bench_batch_c5_default_step_sampled():
+    """bench.py --workload c5's default timed step at N = 1, exactly as bench.py builds it: the
+    8 streams x 512 frames (--frames-per-stream 512, B = 4096: k_pyr_stream, k_rerun's
+    large-batch workgroup count and k_match_init's reduced LDS capacity over 8 x 511 pairs).
+    The device runs the whole step; the oracle checks every 16th within-stream pair plus each
+    stream's last pair, and every frame those pairs touch, bit-exact."""
+    per = 512
+    frames, pairs = _bench_stream_batch(1280, 720, range(8), per)
+    out = _device_extract_and_match(frames, 2500, pairs)
+    nfr, npr = _check_sampled(frames, 2500, per, *out, pairs=pairs)
+    assert nfr >= 8 * 34 and npr >= 8 * 33, (nfr, npr)
+
+
 @pytest.mark.parametrize("rank", [3])
 def test_bench_batch_c5_rank_of_eight_parity(rank):
-    """c5 at N = 8: one rank's load is one stream of 128 frames (B = 128, 127 pairs), below the
-    pyramid-stream and reduced-capacity matcher thresholds: bit-exact."""
-    frames, pairs = _bench_stream_batch(1280, 720, [rank], 128)
+    """c5 at N = 8 as bench.py runs it: one rank's load is one stream of 512 frames (B = 512,
+    511 pairs; replicas.streams_of_rank(8, rank, 8) = [rank]) at 1280x720, which takes
+    k_pyr_stream (B >= 256) and the reduced-capacity matcher (P >= 256) at this geometry.  Every
+    frame and every pair bit-exact."""
+    from orbslam_jpminipc_amd import replicas
+
+    streams = replicas.streams_of_rank(8, rank, 8)
+    assert list(streams) == [rank]
+    frames, pairs = _bench_stream_batch(1280, 720, streams, 512)
     _check_batch(frames, 2500, *_device_extract_and_match(frames, 2500, pairs), pairs=pairs)
 
 

@@ -19,6 +19,9 @@ CAMS = [
     ((718.856, 718.856, 607.1928, 185.2157), (-0.3, 0.1, 0.001, -0.0005)),
     ((320.0, 320.0, 320.0, 240.0), (-0.35, 0.12, -0.002, 0.003)),
     ((500.0, 480.0, 300.5, 260.25), (0.15, -0.02, 0.0, 0.0)),
+    # strong pincushion: keypoints near the edge midpoints undistort outside the corner bounds
+    # (21 of 6 synth frames' keypoints at 640x480, oracle)
+    ((500.0, 480.0, 300.5, 260.25), (0.45, 0.05, 0.0005, 0.0)),
 ]
 
 
@@ -82,11 +85,89 @@ def _check(frames, nf, K4, d4, kps, kun, desc, cnt, m12, nm, bounds):
     assert (nm > 0).all()
 
 
-@pytest.mark.parametrize("W,H,nf,cam", [(640, 480, 1000, 0), (1241, 376, 2000, 1), (752, 480, 1000, 2)])
+@pytest.mark.parametrize("W,H,nf,cam", [(640, 480, 1000, 0), (1241, 376, 2000, 1), (752, 480, 1000, 2),
+                                        (640, 480, 1000, 3), (640, 480, 1000, 4)])
 def test_batch_extract_undistort_match(W, H, nf, cam):
+    """cams 3 / 4 are pincushion cameras (k1 > 0); with cam 4 undistorted keypoints land outside
+    the corner-derived ComputeImageBounds, so k_match_init's PosInGrid rejection on mvKeysUn
+    (Frame.cc:267-277) runs."""
     frames = orb.synth_stream(W, H, stream=31, first=0, count=6)
     K4, d4 = CAMS[cam]
-    _check(frames, nf, K4, d4, *_batch_pipeline(frames, nf, K4, d4))
+    out = _batch_pipeline(frames, nf, K4, d4)
+    _check(frames, nf, K4, d4, *out)
+    if cam == 4:
+        kun, cnt, (x0, x1, y0, y1) = out[1], out[3], out[6]
+        outside = 0
+        for b in range(len(frames)):
+            k = orb.keypoints_from_bytes(kun[b], cnt[b])
+            outside += int(((k["x"] < x0) | (k["x"] >= x1) | (k["y"] < y0) | (k["y"] >= y1)).sum())
+        assert outside > 0  # the out-of-grid rejection really ran
+
+
+@pytest.mark.parametrize("cam", [0, 4])
+def test_batch_undistorted_reduced_capacity(cam):
+    """>= 256 pairs on undistorted keypoints: k_match_init's reduced-LDS-capacity batch (and its
+    in-workgroup large-capacity redo) on mvKeysUn inside the camera's bounds, bit-exact."""
+    import torch
+
+    W, H, nf = 640, 480, 1000
+    K4, d4 = CAMS[cam]
+    frames = orb.synth_stream(W, H, stream=35, first=0, count=8)
+    ext = orb.ORBextractor(nf, 1.2, 8, orb.FAST_SCORE, 20, device=0, max_batch=8)
+    kps, desc, cnt = ext.extract_batch_device(torch.from_numpy(frames).cuda())
+    kun = camera.undistort_keypoints_batch_device(kps, cnt, K4, d4)
+    bounds = camera.image_bounds(W, H, K4, d4)
+    f1 = torch.tensor([b for _ in range(37) for b in range(7)], dtype=torch.int32, device="cuda")
+    assert f1.numel() >= 256
+    m12, nm = orb.ORBmatcher(0.9, True).search_for_initialization_batch_device(kun, desc, cnt, f1, f1 + 1, W, H, 100,
+                                                                               bounds=bounds)
+    torch.cuda.synchronize()
+    kun, desc, cnt, m12, nm = kun.cpu().numpy(), desc.cpu().numpy(), cnt.cpu().numpy(), m12.cpu().numpy(), nm.cpu().numpy()
+    bt = (bounds.min_x, bounds.max_x, bounds.min_y, bounds.max_y)
+    assert bt == compute_image_bounds(W, H, K4, d4)
+    ora = Oracle(nf, 1.2, 8, 1, 20)
+    ref = []
+    for b in range(8):
+        ko, do = ora.extract(frames[b])
+        ku = undistort_keypoints(ko, K4, d4)
+        assert kun[b, : cnt[b]].tobytes() == ku.tobytes(), b
+        ref.append((ku, do))
+    expect = []
+    for b in range(7):
+        (k1, d1), (k2, d2) = ref[b], ref[b + 1]
+        prev = np.ascontiguousarray(np.stack([k1["x"], k1["y"]], 1).astype(np.float32))
+        expect.append(search_for_initialization(k1, d1, k2, d2, W, H, prev, 0.9, True, 100, bounds=bt))
+    for p in range(f1.numel()):
+        no, m12o = expect[p % 7]
+        assert nm[p] == no and np.array_equal(m12[p, : cnt[p % 7]], m12o), p
+    assert (nm > 0).all()
+
+
+def test_pipeline_wrapper_undistorted_pincushion():
+    """FrontEndPipeline.run_undistorted (the Python binding of
+    orb_pipeline_extract_undistort_and_match) with the pincushion camera = oracle."""
+    import torch
+
+    W, H, B, nf = 640, 480, 6, 1000
+    K4, d4 = CAMS[4]
+    frames = orb.synth_stream(W, H, stream=36, first=0, count=B)
+    from orbslam_jpminipc_amd.pipeline import FrontEndPipeline
+
+    pl = FrontEndPipeline(nf, 1.2, 8, orb.FAST_SCORE, 20, device=0, max_batch=B, n_streams=3)
+    cap = pl.max_keypoints
+    d = torch.from_numpy(frames).cuda()
+    kps = torch.empty((B, cap, 28), dtype=torch.uint8, device="cuda")
+    kun = torch.empty_like(kps)
+    desc = torch.empty((B, cap, 32), dtype=torch.uint8, device="cuda")
+    cnt = torch.empty((B,), dtype=torch.int32, device="cuda")
+    m12 = torch.empty((B - 1, cap), dtype=torch.int32, device="cuda")
+    nm = torch.empty((B - 1,), dtype=torch.int32, device="cuda")
+    pl.run_undistorted(d, K4, d4, kps, kun, desc, cnt, m12, nm)
+    torch.cuda.synchronize()
+    pl.close()
+    b = camera.image_bounds(W, H, K4, d4)
+    _check(frames, nf, K4, d4, kps.cpu().numpy(), kun.cpu().numpy(), desc.cpu().numpy(), cnt.cpu().numpy(),
+           m12.cpu().numpy(), nm.cpu().numpy(), (b.min_x, b.max_x, b.min_y, b.max_y))
 
 
 def test_batch_k1_zero_copies():
