@@ -41,6 +41,24 @@
 #ifndef KF_TIMING  // 1: per-phase s_memtime sums of k_fast's waves (experiment builds only)
 #define KF_TIMING 0
 #endif
+#ifndef KR_TIMING  // 1: per-level, per-phase s_memrealtime sums of k_rerun's cell re-runs (experiments)
+#define KR_TIMING 0
+#endif
+#if KR_TIMING
+__device__ unsigned long long g_krtime[ORB_MAX_LEVELS][8];
+#define KR_T(i) const unsigned long long krt##i = __builtin_amdgcn_s_memrealtime()
+#else
+#define KR_T(i)
+#endif
+#ifndef KS_TIMING  // 1: per-level, per-phase s_memrealtime sums of k_select's workgroups (experiments)
+#define KS_TIMING 0
+#endif
+#if KS_TIMING
+__device__ unsigned long long g_kstime[ORB_MAX_LEVELS][8];
+#define KS_T(i) const unsigned long long kst##i = __builtin_amdgcn_s_memrealtime()
+#else
+#define KS_T(i)
+#endif
 #if KF_TIMING
 __device__ unsigned long long g_kftime[8];
 #define KF_T(i) const unsigned long long kft##i = __builtin_amdgcn_s_memrealtime()
@@ -971,8 +989,9 @@ inline size_t rerun_lds(int dw, int dh) {
     return 2 * dwp * dh + 4 * (size_t)((dh + 3) & ~3) + inW * (dh + 6) + 16 + 4 * (4 + 4 * (RR_Q + 8));
 }
 __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int dw, int dh, int rx0, int ry0, int t,
-                               uint8_t* smem, uint32_t* __restrict__ out, int tid) {
+                               uint8_t* smem, uint32_t* __restrict__ out, int tid, int level) {
     const int wave = tid >> 6, lane = tid & 63;
+    KR_T(0);
     const int dwp = (dw + 3) & ~3, rw = dwp >> 2, nw = (dh * dwp) >> 2;
     uint8_t* Sp = smem;
     uint8_t* Fl = Sp + dh * dwp;
@@ -994,6 +1013,7 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
         for (int i = tid; i < dh; i += 256) rowc[i] = 0;
     }
     __syncthreads();
+    KR_T(1);
     // the strength plane (corner at t <=> S > t; the NMS below reads only S > t, so a pixel
     // known not to be a corner may hold 0): per wave, 64 staged dwords (4 pixels each) at a
     // time through the compass test of cv::FAST at t in packed 16-bit arithmetic (compass4, as
@@ -1057,6 +1077,7 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
         }
     }
     __syncthreads();
+    KR_T(2);
     // 3x3 NMS on the corners only: Sp holds S where S > t and 0 elsewhere, so cv::FAST's strict
     // test s0 - 1 > (n > t ? n - 1 : 0) reads the plane as is (out-of-cell neighbours 0).  Each
     // wave scans its share of the plane's dwords, ballot-compacts the nonzero pixels into its
@@ -1114,6 +1135,7 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
         if (cn) nms(cn);
     }
     __syncthreads();
+    KR_T(3);
     __shared__ int s_total;
     if (wave == 0) {
         int carry = 0;
@@ -1150,6 +1172,19 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
         }
     }
     __syncthreads();  // smem is reused by the caller
+#if KR_TIMING
+    // phases: 0 stage + zero, 1 compass + strength, 2 NMS, 3 row scan + output; [4] = cells,
+    // [5] = detection pixels, [6] = corners kept
+    if (tid == 0) {
+        atomicAdd(&g_krtime[level][0], krt1 - krt0);
+        atomicAdd(&g_krtime[level][1], krt2 - krt1);
+        atomicAdd(&g_krtime[level][2], krt3 - krt2);
+        atomicAdd(&g_krtime[level][3], __builtin_amdgcn_s_memrealtime() - krt3);
+        atomicAdd(&g_krtime[level][4], 1ull);
+        atomicAdd(&g_krtime[level][5], (unsigned long long)(dw * dh));
+        atomicAdd(&g_krtime[level][6], (unsigned long long)totalK);
+    }
+#endif
     return totalK;
 }
 
@@ -1204,7 +1239,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KR_WAV
             if (dw > 0 && dh > 0) {
                 const uint8_t* det = pyr + lg.base + (long long)b * lg.fstride +
                                      (long long)(EDGE + cg.y0 + 3) * lg.pitch + EDGE + cg.x0 + 3;
-                n = cell_fast_rerun(det, lg.pitch, dw, dh, cg.x0 + 3, cg.y0 + 3, 7, smem, fcand + cg.candOff, tid);
+                n = cell_fast_rerun(det, lg.pitch, dw, dh, cg.x0 + 3, cg.y0 + 3, 7, smem, fcand + cg.candOff, tid, l);
             }
             if (tid == 0) fcount[cc] = n | RERUN_FLAG;
         }
@@ -1309,6 +1344,7 @@ __device__ __forceinline__ int cell_of(const int* off, int n, int i) {
 #ifndef KS_WAVES
 #define KS_WAVES 2  // waves per SIMD the register allocation targets
 #endif
+
 template <bool HARRIS, bool RERUN>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAVES))) k_select(const uint8_t* __restrict__ pyr, uint32_t* __restrict__ cand,
                                                 uint32_t* __restrict__ cand2, int* __restrict__ cellCount, Geom g,
@@ -1327,6 +1363,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
     // (level, frame) all the heavy level-0 lists landed on one XCD), heaviest level first
     const int b = blockIdx.x, l = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    KS_T(0);
     const LevelGeom& lg = g.lv[l];
     const int nC = lg.rows * lg.cols;
     const CellGeom* lc = cells + lg.cell0;
@@ -1378,7 +1415,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
             if (dw > 0 && dh > 0) {
                 const uint8_t* det = pyr + lg.base + (long long)b * lg.fstride +
                                      (long long)(EDGE + cg.y0 + 3) * lg.pitch + EDGE + cg.x0 + 3;
-                n = cell_fast_rerun(det, lg.pitch, dw, dh, cg.x0 + 3, cg.y0 + 3, 7, smem, fcand + cg.candOff, tid);
+                n = cell_fast_rerun(det, lg.pitch, dw, dh, cg.x0 + 3, cg.y0 + 3, 7, smem, fcand + cg.candOff, tid, l);
             }
             if (tid == 0) {
                 s_cnt[c] = n;
@@ -1387,6 +1424,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
             __syncthreads();
         }
     }
+    KS_T(1);
     if (wave == 0) {
         wave_prefix(s_off, s_cnt, nC, lane);
         // (3) nToRetain / nToDistribute / bNoMore bookkeeping (ORBextractor.cc:622-670), one
@@ -1445,6 +1483,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
             if (64 * j + lane < nC) s_ret[64 * j + lane] = ret[j];
     }
     __syncthreads();
+    KS_T(2);
     const int M = s_off[nC];
     const int selCap = g.selCap;
     const bool inLds = M <= selCap;
@@ -1547,14 +1586,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
         return;
     }
     // (4) retainBest per cell, then the level list in cell order, then retainBest to the quota
+    KS_T(3);
     ScoreGreater comp;
     // cells dealt round-robin over the four waves (cell c on wave c % 4): a level's few dozen
     // serial replays run on four SIMDs instead of one wave's lanes
+    // (measured and dropped, round 4: cells of > 32 / 64 / 128 survivors retained by a whole wave
+    // with the ballot partitions: k_select 71 -> 83-88 us c3, 105 -> 113-122 us c4)
     for (int c = KS_CELL_SPREAD ? lane * 4 + wave : tid; c < nC; c += 256) {
         uint32_t* seg = srt + (inLds ? s_off[c] : lc[c].candOff);
         s_cnt[c] = orbsel::retain_best(seg, s_cnt[c], s_ret[c], comp);
     }
     __syncthreads();
+    KS_T(4);
     if (wave == 0) wave_prefix(s_koff, s_cnt, nC, lane);
     __syncthreads();
     const int K = s_koff[nC];
@@ -1586,9 +1629,24 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
         }
     }
     __syncthreads();
+    KS_T(5);
     uint32_t* out = lvlOut + (long long)b * g.kpCap + lg.kpBase;
     for (int k = tid; k < keep; k += 256) out[k] = list[k];
     if (tid == 0) lvlCount[(long long)b * g.L + l] = keep;
+#if KS_TIMING
+    // phases: 0 counts + re-runs, 1 bookkeeping, 2 load + raster sort, 3 per-cell retainBest,
+    // 4 level list + level retainBest, 5 output; [6] = survivors M, [7] = workgroups
+    if (tid == 0) {
+        atomicAdd(&g_kstime[l][0], kst1 - kst0);
+        atomicAdd(&g_kstime[l][1], kst2 - kst1);
+        atomicAdd(&g_kstime[l][2], kst3 - kst2);
+        atomicAdd(&g_kstime[l][3], kst4 - kst3);
+        atomicAdd(&g_kstime[l][4], kst5 - kst4);
+        atomicAdd(&g_kstime[l][5], __builtin_amdgcn_s_memrealtime() - kst5);
+        atomicAdd(&g_kstime[l][6], (unsigned long long)M);
+        atomicAdd(&g_kstime[l][7], 1ull);
+    }
+#endif
 }
 
 // ---- FAST on the levels: per-tile detection + the per-cell non-max suppression --------------
@@ -1988,11 +2046,29 @@ __device__ __forceinline__ uint32_t blur_round(uint32_t T, bool tail) {
 #ifndef OD_WAVES
 #define OD_WAVES 4  // keypoint slots (waves) per workgroup (8 / 2 measured slower: 0.521 / 0.474 vs 0.468 ms c3)
 #endif
+// Per frame and level: (keypoints of the frame's earlier levels, keypoints of this level) =
+// where the level's keypoints start in the frame's output (level-major, ORBextractor.cc:749-778)
+// and how many there are; and the frame's total (the count the reference returns).  One thread
+// per frame, after k_select: k_orient_desc then reads one pair per wave instead of summing the
+// per-level counts itself.
+__global__ void __launch_bounds__(256) k_lvl_prefix(const int* __restrict__ lvlCount, int L, int B,
+                                                    int2* __restrict__ lvlInfo, int* __restrict__ counts) {
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= B) return;
+    int before = 0;
+    for (int l = 0; l < L; ++l) {
+        const int c = lvlCount[(long long)b * L + l];
+        lvlInfo[(long long)b * ORB_MAX_LEVELS + l] = make_int2(before, c);
+        before += c;
+    }
+    counts[b] = before;
+}
+
 __global__ void __launch_bounds__(64 * OD_WAVES) k_orient_desc(const uint8_t* __restrict__ pyr, Geom g,
                                                      const uint32_t* __restrict__ lvlOut,
-                                                     const int* __restrict__ lvlCount, orb_keypoint_t* __restrict__ kps,
-                                                     uint8_t* __restrict__ desc, int* __restrict__ counts,
-                                                     const float* __restrict__ lvlResp) {
+                                                     const uint8_t* __restrict__ slotLvl,
+                                                     const int2* __restrict__ lvlInfo, orb_keypoint_t* __restrict__ kps,
+                                                     uint8_t* __restrict__ desc, const float* __restrict__ lvlResp) {
     // per wave: the raw window, then (overlaid) the row-pass sums
     __shared__ __attribute__((aligned(16))) uint8_t s_buf[OD_WAVES][OD_BUF];
     __shared__ int2 s_mom[OD_WAVES];     // the waves' IC moments (m01, m10)
@@ -2007,10 +2083,15 @@ __global__ void __launch_bounds__(64 * OD_WAVES) k_orient_desc(const uint8_t* __
     const int k = (bid - b * gridDim.x) * OD_WAVES + wave;  // slot: level l owns [kpBase_l, kpBase_l + nDesired_l)
     // wave-uniform record: x, y and the window base live in SGPRs (its load first: the window's
     // address depends on it)
-    const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane((int)lvlOut[(long long)b * g.kpCap + min(k, g.kpCap - 1)]);
-    int l = 0;
-    for (int i = 1; i < g.L; ++i)
-        if (k >= g.lv[i].kpBase) l = i;
+    const int kc = min(k, g.kpCap - 1);
+    // (32-bit element offsets into the per-slot arrays: the host checks B * kpCap * 32 < 2^32)
+    const uint32_t fslot = (uint32_t)b * (uint32_t)g.kpCap;
+    const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane((int)lvlOut[fslot + (uint32_t)kc]);
+    // the slot's level: one byte of the host-built slot -> level table (a scalar load beside the
+    // record's), then the frame's (first output slot, count) of that level from k_lvl_prefix
+    const uint32_t lw = *(const uint32_t*)(slotLvl + (kc & ~3));
+    const int l = (int)((lw >> (8 * (kc & 3))) & 0xFFu);
+    const int2 linfo = lvlInfo[(uint32_t)b * ORB_MAX_LEVELS + (uint32_t)l];
     const LevelGeom& lg = g.lv[l];
     const int idx = k - lg.kpBase;
     // raw window: padded rows y-5 .. y+37 (level rows y-21 .. y+21), padded columns xa .. xa+63
@@ -2028,6 +2109,8 @@ __global__ void __launch_bounds__(64 * OD_WAVES) k_orient_desc(const uint8_t* __
     uint32_t* Hs = (uint32_t*)s_buf[wave];
     uint32_t icm[5];  // IC_Angle disc masks of the patch dwords this lane reads
     i32x4v Bf[4];  // the row pass's B fragments (constant; in flight with the window loads)
+    // (PC-relative addresses per table load: routing the tables through one opaque SGPR base
+    // saved ~30 SALU per wave but let the loads sink below the window's, 0.420 -> 0.440 ms c3)
 #pragma unroll
     for (int t = 0; t < 4; ++t) Bf[t] = __builtin_bit_cast(i32x4v, c_rowB[t * 64 + lane]);
     constexpr int NU = (2 * OD_WR + 1) * 4;  // 172 16-byte units
@@ -2073,17 +2156,8 @@ __global__ void __launch_bounds__(64 * OD_WAVES) k_orient_desc(const uint8_t* __
             m01 += __mul24(r - HALF_PATCH, S);
         }
     }
-    // output position: level-major order (ORBextractor.cc:749-778); after the window and IC
-    // (scalar loads of the frame's counts: a loop ahead of the window loads delayed them)
-    const int* lc = lvlCount + (long long)b * g.L;
-    int before = 0, cntL = 0, total = 0;
-    for (int i = 0; i < g.L; ++i) {
-        const int c = lc[i];
-        before += i < l ? c : 0;
-        cntL = i == l ? c : cntL;
-        total += c;
-    }
-    if (k == 0 && lane == 0) counts[b] = total;
+    // output position: level-major order (ORBextractor.cc:749-778)
+    const int before = linfo.x, cntL = linfo.y;
     // an empty slot's wave does no work but stays for the workgroup's two barriers
     const bool active = k < g.kpCap && idx < cntL;  // wave-uniform
     // IC_Angle's sums, then the angle arithmetic (fastAtan2, glibc sincosf: ~100 VALU, a fifth of a
@@ -2219,15 +2293,15 @@ __global__ void __launch_bounds__(64 * OD_WAVES) k_orient_desc(const uint8_t* __
 #pragma unroll
     for (int q = 0; q < 4; ++q) nib |= (vals[2 * q] < vals[2 * q + 1]) << q;
     const int other = lane_xor1(nib);
-    const long long kslot = (long long)b * g.kpCap + before + idx;
-    if ((lane & 1) == 0) desc[kslot * 32 + (lane >> 1)] = (uint8_t)(nib | (other << 4));
+    const uint32_t kslot = fslot + (uint32_t)(before + idx);
+    if ((lane & 1) == 0) desc[kslot * 32u + (uint32_t)(lane >> 1)] = (uint8_t)(nib | (other << 4));
     if (lane == 0) {
         orb_keypoint_t kp;
         kp.x = l == 0 ? (float)x : (float)x * lg.scale;
         kp.y = l == 0 ? (float)y : (float)y * lg.scale;
         kp.size = lg.size;
         kp.angle = angle;
-        kp.response = lvlResp ? lvlResp[(long long)b * g.kpCap + k] : (float)score;
+        kp.response = lvlResp ? lvlResp[fslot + (uint32_t)k] : (float)score;
         kp.octave = l;
         kp.class_id = -1;
         kps[kslot] = kp;
@@ -2835,6 +2909,8 @@ struct orb_extractor {
     uint32_t* d_cand2 = nullptr;  // k_select scratch when a level's survivors exceed its LDS
     uint32_t* d_lvl = nullptr;
     int* d_lvlCount = nullptr;
+    int2* d_lvlInfo = nullptr;     // [frame][ORB_MAX_LEVELS] (first output slot, count): k_lvl_prefix
+    uint8_t* d_slotLvl = nullptr;  // keypoint slot -> level (kpCap bytes, padded to a dword)
     uint64_t* d_candH = nullptr;  // HARRIS_SCORE: (response, record) scratch when a level exceeds LDS
     float* d_lvlResp = nullptr;   // HARRIS_SCORE: response of every kept keypoint
     float harrisScale4 = 0.f;
@@ -2887,6 +2963,8 @@ struct orb_extractor {
         hipFree(d_cand2);
         hipFree(d_lvl);
         hipFree(d_lvlCount);
+        hipFree(d_lvlInfo);
+        hipFree(d_slotLvl);
         hipFree(d_candH);
         hipFree(d_lvlResp);
         hipFree(d_rtab);
@@ -2912,6 +2990,8 @@ struct orb_extractor {
         d_cand2 = nullptr;
         d_lvl = nullptr;
         d_lvlCount = nullptr;
+        d_lvlInfo = nullptr;
+        d_slotLvl = nullptr;
         d_candH = nullptr;
         d_lvlResp = nullptr;
         d_rtab = nullptr;
@@ -3192,6 +3272,9 @@ struct orb_extractor {
         G.kpCap = kpCap;
         {  // k_orient_desc's grid is ((kpCap + OD_WAVES - 1) / OD_WAVES, B): bid / gridDim.x by multiply-high
             const unsigned long long gx = (unsigned long long)(std::max(kpCap, 1) + OD_WAVES - 1) / OD_WAVES;
+            // and its per-slot offsets are 32-bit: descriptor bytes of the whole batch < 2^32
+            if ((unsigned long long)std::max(kpCap, 1) * (unsigned long long)maxBatch * 32ull >= (1ull << 32))
+                return set_err(ORB_ENOTSUP, "max_batch x keypoint capacity too large (descriptor bytes >= 4 GiB)");
             G.odDivMagic = (uint32_t)(((1ull << 32) + gx - 1) / gx);
             if (gx * gx * (unsigned long long)maxBatch >= (1ull << 32))
                 return set_err(ORB_ENOTSUP, "keypoint grid too large for k_orient_desc's block decode");
@@ -3228,6 +3311,14 @@ struct orb_extractor {
         HIP_TRY(hipMalloc(&d_cand2, (size_t)std::max(cand, 1) * maxBatch * 4));
         HIP_TRY(hipMalloc(&d_lvl, (size_t)std::max(kpCap, 1) * maxBatch * 4));
         HIP_TRY(hipMalloc(&d_lvlCount, (size_t)nlevels * maxBatch * 4));
+        HIP_TRY(hipMalloc(&d_lvlInfo, (size_t)ORB_MAX_LEVELS * maxBatch * sizeof(int2)));
+        {
+            std::vector<uint8_t> sl(((size_t)std::max(kpCap, 1) + 3) & ~(size_t)3, 0);
+            for (int l = 0; l < nlevels; ++l)
+                for (int k = 0; k < G.lv[l].nDesired; ++k) sl[(size_t)G.lv[l].kpBase + k] = (uint8_t)l;
+            HIP_TRY(hipMalloc(&d_slotLvl, sl.size()));
+            HIP_TRY(hipMemcpy(d_slotLvl, sl.data(), sl.size(), hipMemcpyHostToDevice));
+        }
         if (scoreType == ORB_HARRIS_SCORE) {
             HIP_TRY(hipMalloc(&d_candH, (size_t)std::max(cand, 1) * maxBatch * 8));
             HIP_TRY(hipMalloc(&d_lvlResp, (size_t)std::max(kpCap, 1) * maxBatch * 4));
@@ -3681,11 +3772,14 @@ struct orb_extractor {
                 hipLaunchKernelGGL((k_select<false, true>), sg, dim3(256), selectLds, st, d_pyr, d_cand, d_cand2,
                                    d_cellCount, g, d_cells, d_lvl, d_lvlCount, (uint64_t*)nullptr, (float*)nullptr, 0.f);
         }
+        // the frames' per-level output offsets and totals (part of the selection stage)
+        hipLaunchKernelGGL(k_lvl_prefix, dim3((B + 255) / 256), dim3(256), 0, st, d_lvlCount, nlevels, B, d_lvlInfo,
+                           counts);
         stage_end(3, st);
         stage_begin(4, st);
         dim3 gd((std::max(kpCap, 1) + OD_WAVES - 1) / OD_WAVES, B);
-        hipLaunchKernelGGL(k_orient_desc, gd, dim3(64 * OD_WAVES), 0, st, d_pyr, g, d_lvl, d_lvlCount, kps, desc, counts,
-                           (const float*)d_lvlResp);
+        hipLaunchKernelGGL(k_orient_desc, gd, dim3(64 * OD_WAVES), 0, st, d_pyr, g, d_lvl, d_slotLvl, d_lvlInfo, kps,
+                           desc, (const float*)d_lvlResp);
         stage_end(4, st);
         HIP_TRY(hipGetLastError());
         return ORB_OK;
@@ -4277,6 +4371,26 @@ extern "C" int orb_debug_km_timing(unsigned long long* out8) {
 }
 #endif
 // Per-cell FAST counts (after fallback) of frame `b`, level `l`, row-major cells.
+#if KR_TIMING
+// experiment builds: k_rerun's per-level phase sums, [level][8] (see cell_fast_rerun)
+int orb_debug_kr_timing(unsigned long long* out) {
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_krtime), sizeof(g_krtime)));
+    static unsigned long long z[ORB_MAX_LEVELS][8] = {};
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_krtime), z, sizeof(z)));
+    return ORB_OK;
+}
+#endif
+#if KS_TIMING
+// experiment builds: k_select's per-level phase sums, [level][8] (see the kernel)
+int orb_debug_ks_timing(unsigned long long* out) {
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_kstime), sizeof(g_kstime)));
+    static unsigned long long z[ORB_MAX_LEVELS][8] = {};
+    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_kstime), z, sizeof(z)));
+    return ORB_OK;
+}
+#endif
 #if KF_TIMING
 // experiment builds: k_fast's per-phase s_memtime sums {stage, rows, drain, barrier, nms, waves}
 int orb_debug_kf_timing(unsigned long long* out6) {
