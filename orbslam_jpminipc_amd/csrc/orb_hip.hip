@@ -981,8 +981,11 @@ __device__ __forceinline__ int fast_strength_packed(const uint8_t* p, int TP) {
 // 3 px ring is staged into LDS with dword loads, the strength plane at t = 7 computed, 3x3
 // strict NMS inside the detection region (out-of-region neighbours 0, as cv::FAST on the cell
 // Mat), survivors written in raster order as ((S - 1) << 24) | (y << 12) | x.  Returns the
-// survivor count (all threads).  smem: Sp (dwp x dh) | Fl (dwp x dh) | rowc | In, rerun_lds()
-// bytes.
+// survivor count (all threads).  smem: Sp (dwp x dh) | Bm (survivor bit rows, in a dwp x dh
+// area) | rowc | In, rerun_lds() bytes.  Output: each survivor's record goes to a list in the
+// staged ROI's space (free after the strength pass) and its bit to its row's mask; its raster
+// position is then its row's offset (prefix of the per-row counts) + the set bits before it in
+// its row, so one pass over the list writes every record (no per-row scan of the cell).
 #define RR_Q 320  // per-wave queue of compass survivors (< 64 carried + 4 x 64 new), + a trash slot
 inline size_t rerun_lds(int dw, int dh) {
     const size_t dwp = (size_t)((dw + 3) & ~3), inW = (size_t)((3 + dw + 6 + 3) & ~3);
@@ -994,23 +997,29 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
     KR_T(0);
     const int dwp = (dw + 3) & ~3, rw = dwp >> 2, nw = (dh * dwp) >> 2;
     uint8_t* Sp = smem;
-    uint8_t* Fl = Sp + dh * dwp;
-    int* rowc = (int*)(Fl + dh * dwp);
+    uint32_t* Bm = (uint32_t*)(Sp + dh * dwp);  // survivor bits, bw words per row (<= dwp * dh bytes)
+    const int bw = (dw + 31) >> 5;
+    int* rowc = (int*)((uint8_t*)Bm + dh * dwp);
     uint8_t* In = (uint8_t*)(rowc + ((dh + 3) & ~3));
     const int o = (int)((uintptr_t)(det - 3) & 3);  // dword alignment of the staged ROI
     const int inW = (o + dw + 6 + 3) & ~3;
+    // the survivors' records, in the staged ROI's space once the strength pass is done: (dw + 6)
+    // (dh + 6) bytes hold every survivor of the strict 3x3 NMS (<= ceil(dw / 2) ceil(dh / 2))
+    uint32_t* sl = (uint32_t*)In;
+    __shared__ int s_nsurv;
     {
         const uint32_t* src = (const uint32_t*)(det - 3 * (long long)pitch - 3 - o);
         const int nwr = inW >> 2, pw = pitch >> 2;
         // all loads of a batch in flight before any LDS write (one round trip per 20 dwords
         // per thread, instead of one per row group)
         stage_rows_to_lds<256>((uint32_t*)In, nwr, src, pw, dh + 6, nwr, nwr, tid);
-        // Sp and Fl (contiguous from the 16-B aligned smem) zeroed with 16-B stores: a pixel
-        // the compass rejects keeps strength 0
+        // Sp and Bm's area (contiguous from the 16-B aligned smem) zeroed with 16-B stores: a
+        // pixel the compass rejects keeps strength 0
         const int z16 = (2 * nw) >> 2;
         for (int i = tid; i < z16; i += 256) ((uint4*)Sp)[i] = make_uint4(0u, 0u, 0u, 0u);
         for (int i = 4 * z16 + tid; i < 2 * nw; i += 256) ((uint32_t*)Sp)[i] = 0u;
         for (int i = tid; i < dh; i += 256) rowc[i] = 0;
+        if (tid == 0) s_nsurv = 0;
     }
     __syncthreads();
     KR_T(1);
@@ -1082,7 +1091,8 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
     // test s0 - 1 > (n > t ? n - 1 : 0) reads the plane as is (out-of-cell neighbours 0).  Each
     // wave scans its share of the plane's dwords, ballot-compacts the nonzero pixels into its
     // queue (the strength pass is done with it) and runs the NMS one corner per lane, all nine
-    // reads issued together; a survivor sets its flag and counts into its row (LDS atomics)
+    // reads issued together; a survivor sets its bit, counts into its row (LDS atomics) and
+    // appends its record to the list
     {
         uint32_t* q = (uint32_t*)(In + inW * (dh + 6)) + 4 + wave * (RR_Q + 8);
         const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -1091,6 +1101,8 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
         auto nms = [&](int n) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             for (int k0 = 0; k0 < n; k0 += 64) {
+                bool keep = false;
+                uint32_t rec = 0u;
                 if (k0 + lane < n) {
                     const uint32_t code = q[k0 + lane];
                     const int yy = (int)(code >> 16), xx = (int)(code & 0xFFFFu);
@@ -1102,9 +1114,18 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
                     const int n5 = (yd && xl) ? sp[dwp - 1] : 0, n6 = yd ? sp[dwp] : 0, n7 = (yd && xr) ? sp[dwp + 1] : 0;
                     const int m = max(max(max(n0, n1), max(n2, n3)), max(max(n4, n5), max(n6, n7)));
                     if (s0 > m) {  // s0 > t: a stored strength
-                        Fl[yy * dwp + xx] = 1;
+                        keep = true;
+                        rec = ((uint32_t)(s0 - 1) << 24) | ((uint32_t)(ry0 + yy) << 12) | (uint32_t)(rx0 + xx);
+                        atomicOr(&Bm[yy * bw + (xx >> 5)], 1u << (xx & 31));
                         atomicAdd(&rowc[yy], 1);
                     }
+                }
+                const uint64_t bm = __ballot(keep);
+                if (bm) {  // wave-uniform: one list reservation per 64 candidates
+                    int base = 0;
+                    if (lane == 0) base = atomicAdd(&s_nsurv, (int)__popcll(bm));
+                    base = __builtin_amdgcn_readfirstlane(base);
+                    if (keep) sl[base + __popcll(bm & below)] = rec;
                 }
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1149,27 +1170,16 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
         if (lane == 0) s_total = carry;
     }
     __syncthreads();
-    const uint32_t* Flw = (const uint32_t*)Fl;
     const int totalK = s_total;
-    for (int yy = wave; yy < dh; yy += 4) {
-        int off = rowc[yy];
-        if ((yy + 1 < dh ? rowc[yy + 1] : totalK) == off) continue;  // no survivor in this row
-        const uint32_t ly = (uint32_t)(ry0 + yy) << 12;
-        for (int w0 = 0; w0 < rw; w0 += 64) {
-            const int w = w0 + lane;
-            const uint32_t f = w < rw ? Flw[yy * rw + w] : 0u;
-            const int n = __popc(f);
-            const int incl = wave_incl_scan(n);
-            int pos = off + incl - n;
-#pragma unroll
-            for (int j2 = 0; j2 < 4; ++j2)
-                if ((f >> (8 * j2)) & 1u) {
-                    const int xx = 4 * w + j2;
-                    const uint32_t sc = (uint32_t)(Sp[yy * dwp + xx] - 1);
-                    out[pos++] = (sc << 24) | ly | (uint32_t)(rx0 + xx);
-                }
-            off += __builtin_amdgcn_readlane(incl, 63);
-        }
+    // raster position = the row's offset + the set bits before the survivor in its row
+    for (int i = tid; i < totalK; i += 256) {
+        const uint32_t rec = sl[i];
+        const int yy = (int)((rec >> 12) & 0xFFFu) - ry0, xx = (int)(rec & 0xFFFu) - rx0;
+        const uint32_t* br = Bm + yy * bw;
+        int pos = rowc[yy];
+        for (int w = 0; w < (xx >> 5); ++w) pos += __popc(br[w]);
+        pos += __popc(br[xx >> 5] & ((1u << (xx & 31)) - 1u));
+        out[pos] = rec;
     }
     __syncthreads();  // smem is reused by the caller
 #if KR_TIMING

@@ -12,7 +12,7 @@ step() {  # step NAME RC
     echo "$1 rc=$2" | tee -a $OUT/summary.txt
     if [ "$2" -ne 0 ] && [ "$2" -ne 1 ]; then echo "abnormal end of $1: stopping" | tee -a $OUT/summary.txt; exit "$2"; fi
 }
-timeout -k 10 900 python -u -m pytest tests -q -m gpu --maxfail=5 --timeout 180 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -q -m gpu --maxfail=5 --timeout 180 --timeout-method thread --durations=15 > $OUT/pytest_gpu.log 2>&1
 rc=$?; tail -15 $OUT/pytest_gpu.log >> $OUT/summary.txt; step pytest_gpu $rc
 timeout -k 10 300 python __graft_entry__.py smoke > $OUT/smoke.log 2>&1
 step smoke $?
