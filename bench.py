@@ -450,6 +450,30 @@ def host_fed(ext, matcher, frames_h, f1, f2, W, H, steps, warmup):
 
     h2d_peak = one_way(h_in, d_in[0])
     d2h_peak = one_way(d_in[0], h_in)
+
+    def alone(fn, reps=5):  # one leg of the step by itself, ms per step
+        fn()
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - a) / reps * 1e3
+
+    def compute_leg():
+        with torch.cuda.stream(s_comp):
+            kps, desc, cnt = d_out[0]
+            ext.extract_batch_device(d_in[0], kps, desc, cnt, stream=s_comp)
+            matcher.search_for_initialization_batch_device(kps, desc, cnt, f1, f2, W, H, 100, stream=s_comp)
+
+    def d2h_leg():
+        with torch.cuda.stream(s_d2h):
+            for dst, src in zip(h_out[0], (*d_out[0], *d_m[0])):
+                dst.copy_(src, non_blocking=True)
+
+    h2d_ms = alone(lambda: d_in[0].copy_(h_in, non_blocking=True))
+    comp_ms = alone(compute_leg)
+    d2h_ms = alone(d2h_leg)
     fps = B * steps / dt
     return {
         "value": fps,
@@ -463,6 +487,9 @@ def host_fed(ext, matcher, frames_h, f1, f2, W, H, steps, warmup):
         "h2d_link_GBps_measured": h2d_peak,
         "d2h_link_GBps_measured": d2h_peak,
         "input_bound_fps": h2d_peak * 1e9 / (in_bytes / B),
+        "legs_alone_ms": {"h2d": h2d_ms, "compute": comp_ms, "d2h": d2h_ms,
+                          "sum": h2d_ms + comp_ms + d2h_ms, "max": max(h2d_ms, comp_ms, d2h_ms)},
+        "copy_engine_bound_ms": h2d_ms + d2h_ms,
         "note": f"{B} frames per step from pinned host memory; outputs (keypoint records, descriptors, counts, "
                 f"vnMatches12 of {P} pairs, nmatches) to pinned host memory at full capacity ({cap} slots per frame); "
                 "three streams, double-buffered; link ceilings: one pinned copy of the step's frames each way, alone",
@@ -761,7 +788,8 @@ def run_rank(args):
         result["serial_step"] = {"value": frames_job * args.steps / serial_tmax,
                                  "ms_per_step": serial_tmax / args.steps * 1e3}
     if rank == 0 and world == 1 and args.host_fed:
-        hf = host_fed(ext, matcher, frames, f1, f2, W, H, max(4, args.steps // 2), 2)
+        # (a cold first pass over fresh pinned buffers runs ~1.7x slower: warm up with whole steps)
+        hf = host_fed(ext, matcher, frames, f1, f2, W, H, max(10, args.steps), 8)
         hf["vs_device_resident"] = hf["value"] / value
         result["host_fed"] = hf
     if rank == 0 and world == 1 and args.latency:

@@ -1700,6 +1700,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
 #define FT_Q 512           // per-wave queue (u16 entries): dwords, then the NMS corner list
 #endif
 #define FT_CQ 320          // per-wave pixel list (u16 entries): < 64 carried + 256 expanded
+#ifndef FT_CL
+#define FT_CL 256          // per-wave corner list (u16 entries) filled by the strength passes; a
+                           // workgroup where a wave has more corners scans the strength plane instead
+#endif
 struct FastTile {
     int level, x0, y0;  // detection origin (level coordinates); x0 = 16 + k TW, a multiple of 4
     int tw4, th;        // dwords per row (>= 2), rows (clipped to the detection region)
@@ -1730,6 +1734,8 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
     // unconditionally (no exec-mask branch per append)
     __shared__ uint16_t s_q[4][FT_Q + 2];
     __shared__ uint16_t s_px[4][FT_CQ + 2];  // a chunk's pixels, compacted in place to its corners
+    __shared__ uint16_t s_cl[4][FT_CL + 2];  // the wave's interior corners (tile row << 9 | tile column)
+    __shared__ int s_ovf;                    // a wave's corner list overflowed: scan the plane
     KF_T(0);
 #if KF_XCD
     // XCD-aware order: workgroup i runs on XCD i % 8, so give each XCD a contiguous run of
@@ -1784,6 +1790,7 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
         }
         const int nS = ((t.th + 2) * spw) >> 2;
         for (int i = tid; i < nS; i += 256) ((uint32_t*)s_S)[i] = 0u;
+        if (tid == 0) s_ovf = 0;
     }
     __syncthreads();
     KF_T(1);
@@ -1795,12 +1802,26 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
     // pixel code = plane row << 9 | plane column (plane row = tile row + 1, plane column = tile
     // column + 1); staged byte of a pixel: row pr + 3, column sx + pc - 1
     int np = 0;
+    int ncl = 0;  // the wave's corners so far (wave-uniform)
+    uint16_t* cl = s_cl[wave];
     auto strength_pass = [&](int base, int n) {  // px[base .. base + n), n <= 64
+        bool corner = false;
+        uint16_t code = 0;
         if (lane < n) {
             const uint16_t c = px[base + lane];
             const int S = fast_strength_packed(s_in + ((c >> 9) + 3) * t.sp + t.sx + (c & 511) - 1, t.sp);
             s_S[(c >> 9) * spw + (c & 511) + 3] = (uint8_t)(S > ft ? S : 0);  // each pixel once
+            // an NMS candidate: a corner inside the tile (plane rows 1 .. th, columns 1 .. TW)
+            const int pr = c >> 9, pc = c & 511;
+            corner = S > ft && pr >= 1 && pr <= t.th && pc >= 1 && pc <= 4 * t.tw4;
+            code = (uint16_t)(((pr - 1) << 9) | (pc - 1));
         }
+        const uint64_t m = __ballot(corner);
+        if (corner) {
+            const int ix = ncl + __popcll(m & below);
+            cl[ix < FT_CL ? ix : FT_CL] = code;  // FT_CL: trash slot
+        }
+        ncl += __popcll(m);
     };
     // queue entry = flattened index f << 4 | mask (bit j: pixel j of dword f); f = pr * fw + dc,
     // dword dc - 1 of plane row pr, pixel j at plane column 4 dc + j - 3
@@ -1867,6 +1888,7 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
         drain(qn);
         if (np) strength_pass(0, np);  // the remainder, < 64 pixels
     }
+    if (ncl > FT_CL && lane == 0) s_ovf = 1;
     KF_T(3);
     __syncthreads();
     KF_T(4);
@@ -1875,7 +1897,7 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
     // ((y-16) / cellH, (x-16) / cellW) by exact reciprocal multiplies (host-checked).
     int* fcount = cellCount + (long long)b * g.nCells + lg.cell0;
     uint32_t* fcand = cand + (long long)b * g.candPerFrame + lg.candBase;
-    auto nms_emit = [&](int n) {
+    auto nms_emit = [&](const uint16_t* list, int n) {  // list == pq, or a list disjoint from it
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         int sn = 0;
         for (int k0 = 0; k0 < n; k0 += 64) {
@@ -1883,7 +1905,7 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
             bool keep = false;
             uint16_t e = 0;
             if (k < n) {
-                e = pq[k];
+                e = list[k];
                 const int rt = e >> 9, ct = e & 511;
                 const int X = t.x0 + ct, Y = t.y0 + rt;
                 const int ci = (int)__umulhi((uint32_t)(Y - EDGE), (uint32_t)lg.cellHm);
@@ -1933,9 +1955,12 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     };
-    // the plane's interior corners (ballot-compacted, flattened over th x tw4 dwords), then the
-    // NMS on the list
-    {
+    // the NMS on the wave's own corner list (filled by its strength passes), or, where a wave's
+    // list overflowed, on the plane's interior corners (ballot-compacted, flattened over th x
+    // tw4 dwords) by all waves
+    if (!s_ovf) {
+        if (ncl) nms_emit(cl, ncl);
+    } else {
         int cn = 0;
         const int nI = t.th * t.tw4;
         for (int it = wave; it * 64 < nI; it += 4) {  // wave-uniform
@@ -1956,11 +1981,11 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
                 cn += __popcll(m);
             }
             if (cn > FT_Q - 256) {
-                nms_emit(cn);
+                nms_emit(pq, cn);
                 cn = 0;
             }
         }
-        if (cn) nms_emit(cn);
+        if (cn) nms_emit(pq, cn);
     }
 #if KF_TIMING
     KF_T(5);
@@ -2054,7 +2079,9 @@ __device__ __forceinline__ uint32_t blur_round(uint32_t T, bool tail) {
 }
 
 #ifndef OD_WAVES
-#define OD_WAVES 4  // keypoint slots (waves) per workgroup (8 / 2 measured slower: 0.521 / 0.474 vs 0.468 ms c3)
+#define OD_WAVES 4  // keypoint slots (waves) per workgroup (8 / 2 measured slower: 0.521 / 0.474 vs 0.468 ms c3;
+                    // two slots per wave, lanes 0-31 / 32-63, 2 or 4 waves per workgroup: 0.531 / 0.567 vs
+                    // 0.428 ms c3, 1.018 / 1.093 vs 0.818 c4 -- half the waves per CU, longer chains)
 #endif
 // Per frame and level: (keypoints of the frame's earlier levels, keypoints of this level) =
 // where the level's keypoints start in the frame's output (level-major, ORBextractor.cc:749-778)
@@ -3280,7 +3307,7 @@ struct orb_extractor {
         G.nCells = (int)cl.size();
         G.candPerFrame = cand;
         G.kpCap = kpCap;
-        {  // k_orient_desc's grid is ((kpCap + OD_WAVES - 1) / OD_WAVES, B): bid / gridDim.x by multiply-high
+        {  // k_orient_desc's grid is ((kpCap + slots - 1) / slots, B): bid / gridDim.x by multiply-high
             const unsigned long long gx = (unsigned long long)(std::max(kpCap, 1) + OD_WAVES - 1) / OD_WAVES;
             // and its per-slot offsets are 32-bit: descriptor bytes of the whole batch < 2^32
             if ((unsigned long long)std::max(kpCap, 1) * (unsigned long long)maxBatch * 32ull >= (1ull << 32))
