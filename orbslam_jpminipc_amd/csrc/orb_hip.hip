@@ -900,8 +900,10 @@ __device__ __forceinline__ uint32_t compass4(uint32_t c, uint32_t q0, uint32_t q
         const uint32_t dk = __builtin_bit_cast(uint32_t, (i16x2)(m - (v - t)));  // < 0: dark
         pass[h] = (br | dk) & 0x80008000u;
     }
-    // bit 15 / 31 of even -> pixels 0 / 2, of odd -> pixels 1 / 3
-    return ((pass[0] >> 15) & 1u) | ((pass[1] >> 14) & 2u) | ((pass[0] >> 29) & 4u) | ((pass[1] >> 28) & 8u);
+    // bit 15 / 31 of even -> pixels 0 / 2, of odd -> pixels 1 / 3: bytes (even 1, odd 1, even 3,
+    // odd 3) gathered by one v_perm, their sign bits to bit 0 of each byte, packed by one v_dot4
+    const uint32_t g4 = (__builtin_amdgcn_perm(pass[1], pass[0], 0x07030501u) >> 7) & 0x01010101u;
+    return __builtin_amdgcn_udot4(g4, 0x08040201u, 0u, false);
 }
 
 // ---- FAST strength --------------------------------------------------------------------------
@@ -1736,6 +1738,7 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
     __shared__ uint16_t s_px[4][FT_CQ + 2];  // a chunk's pixels, compacted in place to its corners
     __shared__ uint16_t s_cl[4][FT_CL + 2];  // the wave's interior corners (tile row << 9 | tile column)
     __shared__ int s_ovf;                    // a wave's corner list overflowed: scan the plane
+    __shared__ uint8_t s_cm[FT_TW_MAX / 4 + 2];  // per flattened dword column: its detection pixels
     KF_T(0);
 #if KF_XCD
     // XCD-aware order: workgroup i runs on XCD i % 8, so give each XCD a contiguous run of
@@ -1791,6 +1794,13 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
         const int nS = ((t.th + 2) * spw) >> 2;
         for (int i = tid; i < nS; i += 256) ((uint32_t*)s_S)[i] = 0u;
         if (tid == 0) s_ovf = 0;
+        if (tid < fw) {
+            // dword column dc: pixels X .. X + 3, X = x0 + 4 (dc - 1); the ring columns contribute
+            // the one pixel next to the tile, every pixel inside the detection region [16, detX1)
+            const int dc = tid, X = t.x0 + 4 * (dc - 1);
+            const int lo = max(dc == 0 ? 3 : 0, EDGE - X), hi = min(dc == fw - 1 ? 1 : 4, lg.detX1 - X);
+            s_cm[dc] = (uint8_t)(lo < hi ? (((1u << hi) - 1u) & ~((1u << lo) - 1u)) : 0u);
+        }
     }
     __syncthreads();
     KF_T(1);
@@ -1857,21 +1867,34 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
     {
         int qn = 0;
         const int nF = (t.th + 2) * fw, iw = t.sp >> 2;
-        for (int it = wave; it * 64 < nF; it += 4) {  // wave-uniform
-            const int f = it * 64 + lane;
-            uint32_t mask = 0u;
-            if (f < nF) {
-                const int pr = (int)__umulhi((uint32_t)f, t.rcpF), dc = f - pr * fw;
-                const int Y = t.y0 + pr - 1, X = t.x0 + 4 * (dc - 1);  // level row, column of byte 0
-                // ring dwords contribute their one pixel adjacent to the tile; every pixel must
-                // lie in the level's detection region [16, detX1) x [16, detY1)
-                const int lo = max(dc == 0 ? 3 : 0, EDGE - X), hi = min(dc == fw - 1 ? 1 : 4, lg.detX1 - X);
-                const uint32_t* row = (const uint32_t*)(s_in + (pr + 3) * t.sp + t.sx) + (dc - 1);
-                const uint32_t cc = row[0], lf = row[-1], rg = row[1], up = row[-3 * iw], dn = row[3 * iw];
-                if (Y >= EDGE && Y < lg.detY1 && lo < hi)
-                    mask = compass4(cc, dn, __builtin_amdgcn_alignbyte(rg, cc, 3), up,
-                                    __builtin_amdgcn_alignbyte(cc, lf, 1), tt) &
-                           (((1u << hi) - 1u) & ~((1u << lo) - 1u));
+        // the lane's flattened index f = it * 64 + lane advances by 256 per step: its (plane row,
+        // dword) and staged byte offset are carried instead of divided out each step
+        const int q256 = 256 / fw, r256 = 256 - q256 * fw;  // wave-uniform
+        const int adStep = q256 * t.sp + 4 * r256, adWrap = t.sp - 4 * fw;
+        int f = wave * 64 + lane;
+        int pr = (int)__umulhi((uint32_t)f, t.rcpF), dc = f - pr * fw;
+        int ad = (pr + 3) * t.sp + t.sx + 4 * (dc - 1);  // byte offset of dword dc - 1 of staged row pr + 3
+        const int adSafe = 3 * t.sp + 4;                 // a lane past the end reads row 3, dword 1
+        for (int it = wave; it * 64 < nF; it = __builtin_amdgcn_readfirstlane(it + 4)) {  // wave-uniform
+            const bool valid = f < nF;
+            const int Y = t.y0 + pr - 1;  // level row
+            const uint32_t* row = (const uint32_t*)(s_in + (valid ? ad : adSafe));
+            const uint32_t cc = row[0], lf = row[-1], rg = row[1], up = row[-3 * iw], dn = row[3 * iw];
+            // ring dwords contribute their one pixel adjacent to the tile; every pixel must lie in
+            // the level's detection region [16, detX1) x [16, detY1)
+            const uint32_t cm = s_cm[valid ? dc : 0];
+            uint32_t mask = compass4(cc, dn, __builtin_amdgcn_alignbyte(rg, cc, 3), up,
+                                     __builtin_amdgcn_alignbyte(cc, lf, 1), tt) & cm;
+            mask = (valid && Y >= EDGE && Y < lg.detY1) ? mask : 0u;
+            const int fq = f;
+            f += 256;
+            dc += r256;
+            pr += q256;
+            ad += adStep;
+            if (dc >= fw) {
+                dc -= fw;
+                pr += 1;
+                ad += adWrap;
             }
             if (qn > FT_Q - 64) {
                 drain(qn);
@@ -1879,7 +1902,7 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
             }
             const bool v = mask != 0u;
             const uint64_t m = __ballot(v);
-            pq[v ? qn + __popcll(m & below) : FT_Q] = (uint16_t)(((uint32_t)f << 4) | mask);
+            pq[v ? qn + __popcll(m & below) : FT_Q] = (uint16_t)(((uint32_t)fq << 4) | mask);
             qn += __popcll(m);
         }
 #if KF_TIMING
