@@ -18,5 +18,5 @@ timeout -k 10 300 python __graft_entry__.py smoke > $OUT/smoke.log 2>&1
 step smoke $?
 timeout -k 10 600 python bench.py "$@" > $OUT/bench.json 2> $OUT/bench.err
 step bench $?
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --cpu-frames 0 --latency 0 "$@" > $OUT/prof.log 2>&1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --cpu-frames 0 --latency 0 --host-fed 0 "$@" > $OUT/prof.log 2>&1
 step rocprof $?
