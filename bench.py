@@ -508,8 +508,14 @@ def run_rank(args):
     import orbslam_jpminipc_amd as orb
     from orbslam_jpminipc_amd import replicas
 
-    info = replicas.init_from_env("nccl")
+    # RCCL between one process per GPU; ORB_BENCH_BACKEND=gloo runs the same rank plumbing with
+    # CPU collectives, several ranks sharing a GPU (rank r on device r mod count: the one-GPU
+    # rehearsal of the multi-rank path, tests/test_gpu_replicas.py)
+    backend = os.environ.get("ORB_BENCH_BACKEND", "nccl")
+    info = replicas.init_from_env(backend)
     world, rank, local = info.world, info.rank, info.local_rank
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     wl = WORKLOADS[args.workload]
     W = args.width or wl["W"]

@@ -984,10 +984,10 @@ __device__ __forceinline__ int fast_strength_packed(const uint8_t* p, int TP) {
 // strict NMS inside the detection region (out-of-region neighbours 0, as cv::FAST on the cell
 // Mat), survivors written in raster order as ((S - 1) << 24) | (y << 12) | x.  Returns the
 // survivor count (all threads).  smem: Sp (dwp x dh) | Bm (survivor bit rows, in a dwp x dh
-// area) | rowc | In, rerun_lds() bytes.  Output: each survivor's record goes to a list in the
-// staged ROI's space (free after the strength pass) and its bit to its row's mask; its raster
-// position is then its row's offset (prefix of the per-row counts) + the set bits before it in
-// its row, so one pass over the list writes every record (no per-row scan of the cell).
+// area) | rowc | In, rerun_lds() bytes.  Output: each survivor sets its bit in its row's mask
+// and counts into its row; after the row prefix one thread per mask word writes that word's
+// survivors at the row's offset + the set bits of the row's earlier words (no per-row scan of
+// the cell, no list, no returning atomics in the NMS).
 #define RR_Q 320  // per-wave queue of compass survivors (< 64 carried + 4 x 64 new), + a trash slot
 inline size_t rerun_lds(int dw, int dh) {
     const size_t dwp = (size_t)((dw + 3) & ~3), inW = (size_t)((3 + dw + 6 + 3) & ~3);
@@ -1005,10 +1005,6 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
     uint8_t* In = (uint8_t*)(rowc + ((dh + 3) & ~3));
     const int o = (int)((uintptr_t)(det - 3) & 3);  // dword alignment of the staged ROI
     const int inW = (o + dw + 6 + 3) & ~3;
-    // the survivors' records, in the staged ROI's space once the strength pass is done: (dw + 6)
-    // (dh + 6) bytes hold every survivor of the strict 3x3 NMS (<= ceil(dw / 2) ceil(dh / 2))
-    uint32_t* sl = (uint32_t*)In;
-    __shared__ int s_nsurv;
     {
         const uint32_t* src = (const uint32_t*)(det - 3 * (long long)pitch - 3 - o);
         const int nwr = inW >> 2, pw = pitch >> 2;
@@ -1021,7 +1017,6 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
         for (int i = tid; i < z16; i += 256) ((uint4*)Sp)[i] = make_uint4(0u, 0u, 0u, 0u);
         for (int i = 4 * z16 + tid; i < 2 * nw; i += 256) ((uint32_t*)Sp)[i] = 0u;
         for (int i = tid; i < dh; i += 256) rowc[i] = 0;
-        if (tid == 0) s_nsurv = 0;
     }
     __syncthreads();
     KR_T(1);
@@ -1103,8 +1098,6 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
         auto nms = [&](int n) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             for (int k0 = 0; k0 < n; k0 += 64) {
-                bool keep = false;
-                uint32_t rec = 0u;
                 if (k0 + lane < n) {
                     const uint32_t code = q[k0 + lane];
                     const int yy = (int)(code >> 16), xx = (int)(code & 0xFFFFu);
@@ -1116,18 +1109,9 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
                     const int n5 = (yd && xl) ? sp[dwp - 1] : 0, n6 = yd ? sp[dwp] : 0, n7 = (yd && xr) ? sp[dwp + 1] : 0;
                     const int m = max(max(max(n0, n1), max(n2, n3)), max(max(n4, n5), max(n6, n7)));
                     if (s0 > m) {  // s0 > t: a stored strength
-                        keep = true;
-                        rec = ((uint32_t)(s0 - 1) << 24) | ((uint32_t)(ry0 + yy) << 12) | (uint32_t)(rx0 + xx);
                         atomicOr(&Bm[yy * bw + (xx >> 5)], 1u << (xx & 31));
                         atomicAdd(&rowc[yy], 1);
                     }
-                }
-                const uint64_t bm = __ballot(keep);
-                if (bm) {  // wave-uniform: one list reservation per 64 candidates
-                    int base = 0;
-                    if (lane == 0) base = atomicAdd(&s_nsurv, (int)__popcll(bm));
-                    base = __builtin_amdgcn_readfirstlane(base);
-                    if (keep) sl[base + __popcll(bm & below)] = rec;
                 }
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1173,15 +1157,22 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
     }
     __syncthreads();
     const int totalK = s_total;
-    // raster position = the row's offset + the set bits before the survivor in its row
-    for (int i = tid; i < totalK; i += 256) {
-        const uint32_t rec = sl[i];
-        const int yy = (int)((rec >> 12) & 0xFFFu) - ry0, xx = (int)(rec & 0xFFFu) - rx0;
+    // one thread per mask word: its survivors' raster positions start at the row's offset + the
+    // set bits of the row's earlier words (each record: the stored strength and the position)
+    for (int i = tid; i < dh * bw; i += 256) {
+        uint32_t m = Bm[i];
+        if (!m) continue;
+        const int yy = i / bw, w = i - yy * bw;
         const uint32_t* br = Bm + yy * bw;
         int pos = rowc[yy];
-        for (int w = 0; w < (xx >> 5); ++w) pos += __popc(br[w]);
-        pos += __popc(br[xx >> 5] & ((1u << (xx & 31)) - 1u));
-        out[pos] = rec;
+        for (int w2 = 0; w2 < w; ++w2) pos += __popc(br[w2]);
+        const uint32_t ly = (uint32_t)(ry0 + yy) << 12;
+        while (m) {
+            const int xx = 32 * w + __builtin_ctz(m);
+            m &= m - 1;
+            const uint32_t sc = (uint32_t)(Sp[yy * dwp + xx] - 1);
+            out[pos++] = (sc << 24) | ly | (uint32_t)(rx0 + xx);
+        }
     }
     __syncthreads();  // smem is reused by the caller
 #if KR_TIMING
@@ -1696,8 +1687,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
 #define FT_IN_BYTES 12672  // staged-tile LDS budget (44 rows of 288 B at TW = 256)
 #endif
 #ifndef FT_S_BYTES
-#define FT_S_BYTES 10032   // strength-plane LDS budget (38 rows of 264 B at TW = 256)
+#define FT_S_BYTES 10032   // strength-plane LDS budget (38 rows of 264 B at TW = 256; a multiple of 16)
 #endif
+static_assert(FT_S_BYTES % 16 == 0 && FT_IN_BYTES % 16 == 0, "k_fast's LDS buffers are cleared / staged in 16-B units");
 #ifndef FT_Q
 #define FT_Q 512           // per-wave queue (u16 entries): dwords, then the NMS corner list
 #endif
@@ -1791,8 +1783,9 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
             const int i = tid + 256 * k;
             if (i < nU) ((uint4*)s_in)[i] = v[k];
         }
-        const int nS = ((t.th + 2) * spw) >> 2;
-        for (int i = tid; i < nS; i += 256) ((uint32_t*)s_S)[i] = 0u;
+        // the strength plane zeroed with 16-B stores (FT_S_BYTES is a multiple of 16)
+        const int nS = ((t.th + 2) * spw + 15) >> 4;
+        for (int i = tid; i < nS; i += 256) ((uint4*)s_S)[i] = make_uint4(0u, 0u, 0u, 0u);
         if (tid == 0) s_ovf = 0;
         if (tid < fw) {
             // dword column dc: pixels X .. X + 3, X = x0 + 4 (dc - 1); the ring columns contribute
