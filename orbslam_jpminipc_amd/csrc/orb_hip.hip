@@ -1707,8 +1707,8 @@ struct FastTile {
 #define KF_XCD 0  // 1: XCD-aware workgroup order; measured slower (0.646 vs 0.574 ms c3, 0.913
                   // vs 0.832 c4, 1.627 vs 1.557 720p): the halo re-reads are not what binds
 #endif
-#ifndef KF_PAIR
-#define KF_PAIR 0  // 1: the compass loop takes two adjacent dwords per lane and step
+#ifndef KF_DPL
+#define KF_DPL 2  // adjacent dwords per lane and step of the compass loop (1, 2 or 4)
 #endif
 #ifndef KF_WAVES
 #define KF_WAVES 0  // > 0: waves per SIMD the register allocation targets
@@ -1729,7 +1729,8 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
     __shared__ uint16_t s_px[4][FT_CQ + 2];  // a chunk's pixels, compacted in place to its corners
     __shared__ uint16_t s_cl[4][FT_CL + 2];  // the wave's interior corners (tile row << 9 | tile column)
     __shared__ int s_ovf;                    // a wave's corner list overflowed: scan the plane
-    __shared__ uint8_t s_cm[FT_TW_MAX / 4 + 3];  // per flattened dword column: its detection pixels
+    __shared__ uint8_t s_cm[FT_TW_MAX / 4 + 2 + KF_DPL];  // per flattened dword column: its detection
+                                                           // pixels (0 past the ring)
     KF_T(0);
 #if KF_XCD
     // XCD-aware order: workgroup i runs on XCD i % 8, so give each XCD a contiguous run of
@@ -1793,7 +1794,7 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
             const int lo = max(dc == 0 ? 3 : 0, EDGE - X), hi = min(dc == fw - 1 ? 1 : 4, lg.detX1 - X);
             s_cm[dc] = (uint8_t)(lo < hi ? (((1u << hi) - 1u) & ~((1u << lo) - 1u)) : 0u);
         }
-        if (tid == fw) s_cm[fw] = 0;  // the pair loop's dword past the ring
+        if (tid >= fw && tid < fw + KF_DPL) s_cm[tid] = 0;  // the compass groups' dwords past the ring
     }
     __syncthreads();
     KF_T(1);
@@ -1857,57 +1858,61 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
 #if KF_TIMING
     unsigned long long kft2 = 0;
 #endif
-#if KF_PAIR
     {
-        // two adjacent dwords (8 pixels) per lane and step: the pair shares its left / centre /
-        // right loads and the step bookkeeping.  Pair index g = pr * fwp + k over the plane rows
-        // whose level row lies in the detection region (only the two ring rows can fall outside,
-        // so the region test is the loop's row range); pair k covers dwords 2k, 2k + 1 (dword fw,
-        // past the ring when fw is odd, has no detection pixel: s_cm[fw] = 0)
+        // KF_DPL adjacent dwords (4 KF_DPL pixels) per lane and step: a group shares its left /
+        // centre / right loads and the step bookkeeping (one dword per lane before: 484 -> 466 us
+        // per 512 c3 frames with two, 700 -> 669 c4, 9.52 -> 8.95 ms per 4096 720p).  Group
+        // index g = pr * fwg + k over the plane rows whose level row lies in the detection region
+        // (only the two ring rows can fall outside, so the region test is the loop's row range);
+        // group k covers dwords KF_DPL k .. KF_DPL k + KF_DPL - 1 (those past the ring, fw ..,
+        // have no detection pixel: s_cm is 0 there)
         int qn = 0;
-        const int iw = t.sp >> 2, fwp = (fw + 1) >> 1;
+        const int iw = t.sp >> 2, fwg = (fw + KF_DPL - 1) / KF_DPL;
         const int prLo = max(0, EDGE + 1 - t.y0), prHi = min(t.th + 2, lg.detY1 + 1 - t.y0);  // wave-uniform
-        const int nP = (prHi - prLo) * fwp;
-        const int q256 = 256 / fwp, r256 = 256 - q256 * fwp;
-        const int adStep = q256 * t.sp + 8 * r256, adWrap = t.sp - 8 * fwp;
+        const int nP = (prHi - prLo) * fwg;
+        const int q256 = 256 / fwg, r256 = 256 - q256 * fwg;
+        const int adStep = q256 * t.sp + 4 * KF_DPL * r256, adWrap = t.sp - 4 * KF_DPL * fwg;
         int g = wave * 64 + lane;
-        int pr = g / fwp, kp = g - pr * fwp;
+        int pr = g / fwg, kp = g - pr * fwg;
         pr += prLo;
-        int ad = (pr + 3) * t.sp + t.sx + 4 * (2 * kp - 1);  // byte offset of dword 2k - 1 of staged row pr + 3
+        int ad = (pr + 3) * t.sp + t.sx + 4 * (KF_DPL * kp - 1);  // byte offset of the group's first dword
         const int adSafe = 3 * t.sp + 4;
         for (int it = wave; it * 64 < nP; it = __builtin_amdgcn_readfirstlane(it + 4)) {  // wave-uniform
             const bool valid = g < nP;
             const uint32_t* row = (const uint32_t*)(s_in + (valid ? ad : adSafe));
-            const uint32_t lf = row[-1], c0 = row[0], c1 = row[1], rg = row[2];
-            const uint32_t up0 = row[-3 * iw], up1 = row[1 - 3 * iw], dn0 = row[3 * iw], dn1 = row[3 * iw + 1];
-            const int dc = valid ? 2 * kp : 0;
-            const uint32_t cm0 = s_cm[dc], cm1 = s_cm[dc + 1];
-            uint32_t m0 = compass4(c0, dn0, __builtin_amdgcn_alignbyte(c1, c0, 3), up0,
-                                   __builtin_amdgcn_alignbyte(c0, lf, 1), tt) & cm0;
-            uint32_t m1 = compass4(c1, dn1, __builtin_amdgcn_alignbyte(rg, c1, 3), up1,
-                                   __builtin_amdgcn_alignbyte(c1, c0, 1), tt) & cm1;
-            m0 = valid ? m0 : 0u;
-            m1 = valid ? m1 : 0u;
-            const int fq = pr * fw + 2 * kp;
+            uint32_t h[KF_DPL + 2];  // dwords -1 .. KF_DPL of the group's row
+#pragma unroll
+            for (int j = 0; j < KF_DPL + 2; ++j) h[j] = row[j - 1];
+            const int dc = valid ? KF_DPL * kp : 0;
+            const int fq = pr * fw + KF_DPL * kp;
+            uint32_t m[KF_DPL];
+#pragma unroll
+            for (int j = 0; j < KF_DPL; ++j) {
+                const uint32_t up = row[j - 3 * iw], dn = row[j + 3 * iw];
+                m[j] = compass4(h[j + 1], dn, __builtin_amdgcn_alignbyte(h[j + 2], h[j + 1], 3), up,
+                                __builtin_amdgcn_alignbyte(h[j + 1], h[j], 1), tt) & s_cm[dc + j];
+                m[j] = valid ? m[j] : 0u;
+            }
             g += 256;
             kp += r256;
             pr += q256;
             ad += adStep;
-            if (kp >= fwp) {
-                kp -= fwp;
+            if (kp >= fwg) {
+                kp -= fwg;
                 pr += 1;
                 ad += adWrap;
             }
-            if (qn > FT_Q - 128) {
+            if (qn > FT_Q - 64 * KF_DPL) {
                 drain(qn);
                 qn = 0;
             }
-            const bool v0 = m0 != 0u, v1 = m1 != 0u;
-            const uint64_t b0 = __ballot(v0), b1 = __ballot(v1);
-            const int n0 = (int)__popcll(b0);
-            pq[v0 ? qn + __popcll(b0 & below) : FT_Q] = (uint16_t)(((uint32_t)fq << 4) | m0);
-            pq[v1 ? qn + n0 + __popcll(b1 & below) : FT_Q] = (uint16_t)(((uint32_t)(fq + 1) << 4) | m1);
-            qn += n0 + (int)__popcll(b1);
+#pragma unroll
+            for (int j = 0; j < KF_DPL; ++j) {
+                const bool v = m[j] != 0u;
+                const uint64_t bm = __ballot(v);
+                pq[v ? qn + __popcll(bm & below) : FT_Q] = (uint16_t)(((uint32_t)(fq + j) << 4) | m[j]);
+                qn += (int)__popcll(bm);
+            }
         }
 #if KF_TIMING
         kft2 = __builtin_amdgcn_s_memrealtime();
@@ -1915,55 +1920,6 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
         drain(qn);
         if (np) strength_pass(0, np);  // the remainder, < 64 pixels
     }
-#else
-    {
-        int qn = 0;
-        const int nF = (t.th + 2) * fw, iw = t.sp >> 2;
-        // the lane's flattened index f = it * 64 + lane advances by 256 per step: its (plane row,
-        // dword) and staged byte offset are carried instead of divided out each step
-        const int q256 = 256 / fw, r256 = 256 - q256 * fw;  // wave-uniform
-        const int adStep = q256 * t.sp + 4 * r256, adWrap = t.sp - 4 * fw;
-        int f = wave * 64 + lane;
-        int pr = (int)__umulhi((uint32_t)f, t.rcpF), dc = f - pr * fw;
-        int ad = (pr + 3) * t.sp + t.sx + 4 * (dc - 1);  // byte offset of dword dc - 1 of staged row pr + 3
-        const int adSafe = 3 * t.sp + 4;                 // a lane past the end reads row 3, dword 1
-        for (int it = wave; it * 64 < nF; it = __builtin_amdgcn_readfirstlane(it + 4)) {  // wave-uniform
-            const bool valid = f < nF;
-            const int Y = t.y0 + pr - 1;  // level row
-            const uint32_t* row = (const uint32_t*)(s_in + (valid ? ad : adSafe));
-            const uint32_t cc = row[0], lf = row[-1], rg = row[1], up = row[-3 * iw], dn = row[3 * iw];
-            // ring dwords contribute their one pixel adjacent to the tile; every pixel must lie in
-            // the level's detection region [16, detX1) x [16, detY1)
-            const uint32_t cm = s_cm[valid ? dc : 0];
-            uint32_t mask = compass4(cc, dn, __builtin_amdgcn_alignbyte(rg, cc, 3), up,
-                                     __builtin_amdgcn_alignbyte(cc, lf, 1), tt) & cm;
-            mask = (valid && Y >= EDGE && Y < lg.detY1) ? mask : 0u;
-            const int fq = f;
-            f += 256;
-            dc += r256;
-            pr += q256;
-            ad += adStep;
-            if (dc >= fw) {
-                dc -= fw;
-                pr += 1;
-                ad += adWrap;
-            }
-            if (qn > FT_Q - 64) {
-                drain(qn);
-                qn = 0;
-            }
-            const bool v = mask != 0u;
-            const uint64_t m = __ballot(v);
-            pq[v ? qn + __popcll(m & below) : FT_Q] = (uint16_t)(((uint32_t)fq << 4) | mask);
-            qn += __popcll(m);
-        }
-#if KF_TIMING
-        kft2 = __builtin_amdgcn_s_memrealtime();
-#endif
-        drain(qn);
-        if (np) strength_pass(0, np);  // the remainder, < 64 pixels
-    }
-#endif
     if (ncl > FT_CL && lane == 0) s_ovf = 1;
     KF_T(3);
     __syncthreads();
