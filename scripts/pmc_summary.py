@@ -20,7 +20,7 @@ import json
 from collections import defaultdict
 
 
-WIDE_LOADS = {"k_pyr0", "k_pyr_stream", "k_pyr_resize", "k_fast", "k_orient_desc"}
+WIDE_LOADS = {"k_pyr0", "k_pyr_stream", "k_pyr_resize", "k_fast", "k_orient_desc", "k_rerun"}  # k_rerun: round 4
 
 
 def main():
