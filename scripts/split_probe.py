@@ -24,7 +24,7 @@ f1 = torch.arange(B - 1, dtype=torch.int32, device="cuda")
 f2 = f1 + 1
 
 
-def run(S, steps=30, warm=5):
+def run(S, steps=30, warm=5, offset=False):
     exts = [orb.ORBextractor(NF, 1.2, 8, orb.FAST_SCORE, 20, device=0, max_batch=B // S) for _ in range(S)]
     cap = exts[0].max_keypoints
     d_kps = torch.empty((B, cap, 28), dtype=torch.uint8, device="cuda")
@@ -35,12 +35,25 @@ def run(S, steps=30, warm=5):
     s0 = streams[0]
     h = B // S
 
+    ev_pyr = [torch.cuda.Event() for _ in range(S)]
+
     def step():
         for i, (e, s) in enumerate(zip(exts, streams)):
+            # offset: sub-batch i starts its pyramid when sub-batch i-1's pyramid is done, so a
+            # pyramid overlaps the previous sub-batch's detection and descriptors
             if i:
-                s.wait_event(ev_start)
-            e.extract_batch_device(d_imgs[i * h:(i + 1) * h], d_kps[i * h:(i + 1) * h], d_desc[i * h:(i + 1) * h],
-                                   d_cnt[i * h:(i + 1) * h], stream=s)
+                s.wait_event(ev_pyr[i - 1] if offset else ev_start)
+            args = (d_imgs[i * h:(i + 1) * h], d_kps[i * h:(i + 1) * h], d_desc[i * h:(i + 1) * h],
+                    d_cnt[i * h:(i + 1) * h])
+            if offset:
+                e.set_phases(1)
+                e.extract_batch_device(*args, stream=s)
+                ev_pyr[i].record(s)
+                e.set_phases(2)
+                e.extract_batch_device(*args, stream=s)
+                e.set_phases(3)
+            else:
+                e.extract_batch_device(*args, stream=s)
             ev[i].record(s)
         for i in range(1, S):
             s0.wait_event(ev[i])
@@ -63,7 +76,8 @@ def run(S, steps=30, warm=5):
 
 ref = run(1)
 print(f"{W}x{H} nf={NF} B={B}: 1 stream {ref[0]:.3f} ms/step ({B / ref[0] * 1e3:.0f} frames/s)")
-for S in (2, 4):
-    r = run(S)
+for S, off in ((2, False), (2, True), (4, True)):
+    r = run(S, offset=off)
     same = all(torch.equal(a, b) for a, b in zip(ref[1:], r[1:]))
-    print(f"  {S} streams {r[0]:.3f} ms/step ({B / r[0] * 1e3:.0f} frames/s), outputs identical: {same}")
+    print(f"  {S} streams{' offset' if off else ''} {r[0]:.3f} ms/step ({B / r[0] * 1e3:.0f} frames/s), "
+          f"outputs identical: {same}")
