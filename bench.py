@@ -59,6 +59,12 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# HIP maps streams round-robin onto GPU_MAX_HW_QUEUES hardware queues (4 by default): the
+# host-fed leg's three streams then share queues with the streams created before them and its
+# H2D copies serialise with the extraction (4.18 ms per c3 step = H2D + compute).  Eight
+# queues give every stream its own: 3.12 ms (profiles/r04_hostfed_queues.txt).  Set before any
+# HIP call, inherited by the rank processes.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md §Chip-level parameters)
 N_CU, CLOCK_HZ = 256, 2.4e9
