@@ -64,7 +64,8 @@ sys.path.insert(0, ROOT)
 # H2D copies serialise with the extraction (4.18 ms per c3 step = H2D + compute).  Eight
 # queues give every stream its own: 3.12 ms (profiles/r04_hostfed_queues.txt).  Set before any
 # HIP call, inherited by the rank processes.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+if int(os.environ.get("GPU_MAX_HW_QUEUES") or 0) < 8:  # the boxes export 4
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md §Chip-level parameters)
 N_CU, CLOCK_HZ = 256, 2.4e9
