@@ -3,7 +3,7 @@
 test_extract_parity_configs[W-H-nf] with the library named by ORB_HIP_LIB (or the in-tree one)
 and the oracle, and print, per differing descriptor row, the keypoint, its window alignment and
 the differing rBRIEF tests (test i = pattern points 2i, 2i+1; lane i // 4 of k_orient_desc).
-Usage: od_diag.py [W H nf]"""
+Usage: od_diag.py [W H nf [reps]]"""
 import pathlib
 import sys
 
@@ -16,11 +16,12 @@ import orbslam_jpminipc_amd as orb  # noqa: E402
 from oracle_lib import Oracle  # noqa: E402
 
 W, H, NF = (int(x) for x in (sys.argv[1:4] if len(sys.argv) >= 4 else (640, 480, 2000)))
+REPS = int(sys.argv[4]) if len(sys.argv) >= 5 else 6
 ext = orb.ORBextractor(NF, 1.2, 8, orb.FAST_SCORE, 20, device=0)
 ora = Oracle(NF, 1.2, 8, 1, 20)
 tot = 0
 for fi, img in enumerate(orb.synth_stream(W, H, stream=3, first=0, count=3)):
-    for rep in range(6):
+    for rep in range(REPS):
         kg, dg = ext(img)
         ko, do = ora.extract(img)
         if kg.tobytes() != ko.tobytes():
