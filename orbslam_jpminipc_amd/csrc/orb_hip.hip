@@ -941,7 +941,7 @@ __device__ __forceinline__ int fast_strength_packed(const uint8_t* p, int TP) {
 
 // The reference's `FAST(cellImage, keys, 7, true)` re-run of a cell that kept <= 3 corners at
 // fastTh (ORBextractor.cc:609-614), by a whole 256-thread workgroup: the cell ROI with its
-// 3 px ring is staged into LDS with dword loads, the strength plane at t = 7 computed, 3x3
+// 3 px ring is staged into LDS with 16-byte loads, the strength plane at t = 7 computed, 3x3
 // strict NMS inside the detection region (out-of-region neighbours 0, as cv::FAST on the cell
 // Mat), survivors written in raster order as ((S - 1) << 24) | (y << 12) | x.  Returns the
 // survivor count (all threads).  smem: Sp (dwp x dh, 16-B padded) | Bm (dh x bw survivor mask
