@@ -3349,7 +3349,8 @@ struct orb_extractor {
                 return set_err(ORB_ENOTSUP, "keypoint grid too large for k_orient_desc's block decode");
         }
         // workspace
-        // + slack: k_orient_desc's 64-byte window rows may over-read the last row's pitch
+        // + slack: k_orient_desc's 64-byte window rows and k_rerun's 16-B ROI units may over-read
+        // the last row's pitch
         HIP_TRY(hipMalloc(&d_pyr, (size_t)pyrBytes + 256));
         // k_fast tiles over each level's detection region: the width split evenly into
         // ceil(width / 256) tiles of a multiple of 4 columns, as many rows as the LDS budgets
