@@ -59,13 +59,6 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-# HIP maps streams round-robin onto GPU_MAX_HW_QUEUES hardware queues (4 by default): the
-# host-fed leg's three streams then share queues with the streams created before them and its
-# H2D copies serialise with the extraction (4.18 ms per c3 step = H2D + compute).  Eight
-# queues give every stream its own: 3.12 ms (profiles/r04_hostfed_queues.txt).  Set before any
-# HIP call, inherited by the rank processes.
-if int(os.environ.get("GPU_MAX_HW_QUEUES") or 0) < 8:  # the boxes export 4
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md §Chip-level parameters)
 N_CU, CLOCK_HZ = 256, 2.4e9
@@ -280,7 +273,7 @@ def run_dry(args):
     import orbslam_jpminipc_amd as orb
     from orbslam_jpminipc_amd import replicas
 
-    info = replicas.init_from_env("gloo")
+    info = replicas.init_from_env()  # the default control plane (gloo)
     W, H, B = 160, 120, 2
     frames = orb.synth_stream(W, H, stream=info.rank, first=0, count=B)
     ora = Oracle(300, 1.2, 4, 1, 20)
@@ -403,7 +396,14 @@ def host_fed(ext, matcher, frames_h, f1, f2, W, H, steps, warmup):
               torch.empty((B,), dtype=torch.int32).pin_memory(),
               torch.empty((P, cap), dtype=torch.int32).pin_memory(),
               torch.empty((P,), dtype=torch.int32).pin_memory()) for _ in range(2)]
-    s_h2d, s_comp, s_d2h = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+    # HIP maps plain streams round-robin onto GPU_MAX_HW_QUEUES hardware queues (4 by default):
+    # three plain streams here share queues with the streams created before them and the H2D
+    # copies serialise with the extraction (4.18 ms per c3 step = H2D + compute, round 4).  The
+    # library's dedicated-queue streams avoid that at the default queue count
+    from orbslam_jpminipc_amd.streams import dedicated_stream
+
+    dev = torch.cuda.current_device()
+    s_h2d, s_comp, s_d2h = dedicated_stream(dev), dedicated_stream(dev), dedicated_stream(dev)
     ev_h2d = [torch.cuda.Event() for _ in range(2)]
     ev_comp = [torch.cuda.Event() for _ in range(2)]
     ev_d2h = [torch.cuda.Event() for _ in range(2)]
@@ -505,7 +505,7 @@ def host_fed(ext, matcher, frames_h, f1, f2, W, H, steps, warmup):
         "passes_ms_per_step": [x / steps * 1e3 for x in passes],
         "note": f"{B} frames per step from pinned host memory; outputs (keypoint records, descriptors, counts, "
                 f"vnMatches12 of {P} pairs, nmatches) to pinned host memory at full capacity ({cap} slots per frame); "
-                "three streams, double-buffered; link ceilings: one pinned copy of the step's frames each way, alone",
+                "three dedicated-queue streams (orb_stream_create_dedicated), double-buffered; link ceilings: one pinned copy of the step's frames each way, alone",
     }
 
 
@@ -515,15 +515,18 @@ def run_rank(args):
     import orbslam_jpminipc_amd as orb
     from orbslam_jpminipc_amd import replicas
 
-    # RCCL between one process per GPU; ORB_BENCH_BACKEND=gloo runs the same rank plumbing with
-    # CPU collectives, several ranks sharing a GPU (rank r on device r mod count: the one-GPU
-    # rehearsal of the multi-rank path, tests/test_gpu_replicas.py)
-    backend = os.environ.get("ORB_BENCH_BACKEND", "nccl")
+    # The control plane (barrier, max over ranks, gather of the per-rank seconds) runs on gloo
+    # by default: the path has no data-path collective, so RCCL would only add
+    # its init on every rank; gloo is the backend tests/test_multiproc.py and
+    # tests/test_gpu_replicas.py rehearse.  ORB_BENCH_BACKEND=nccl selects RCCL.  Rank r uses
+    # device r mod count (several ranks share the one GPU of a test box).
+    backend = os.environ.get("ORB_BENCH_BACKEND", "gloo")
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 and backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())  # device_count does not initialise the GPU
+    torch.cuda.set_device(local)  # before the process group and before any other GPU call
     info = replicas.init_from_env(backend)
-    world, rank, local = info.world, info.rank, info.local_rank
-    if backend != "nccl":
-        local = local % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local)
+    world, rank = info.world, info.rank
     wl = WORKLOADS[args.workload]
     W = args.width or wl["W"]
     H = args.height or wl["H"]
@@ -757,6 +760,8 @@ def run_rank(args):
             "pairs_per_gpu": P,
             "streams_of_rank0": my_streams,
             "parallelism": f"replicas x{world} (no collectives)",
+            "control_backend": backend if world > 1 else None,
+            "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
             "streams": {0: "one stream, extract then match",
                         1: "extract(t) || SearchForInitialization(t-1), double-buffered",
                         2: "pyramid(t) || SearchForInitialization(t-1), then the rest of extract(t)"}

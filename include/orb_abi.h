@@ -153,6 +153,17 @@ int orb_search_for_initialization_batch_device(const orb_keypoint_t* d_kps, cons
  * orb_search_for_initialization_batch_device; a later call on the stream re-creates it.  No
  * reference counterpart (resource hook of the batched entry point). */
 int orb_match_release_stream_scratch(void* stream);
+/* A HIP stream on the current device with a hardware queue of its own, for callers that
+ * overlap H2D copies, extraction and D2H copies on separate streams (the host-fed step of
+ * ORBextractor::operator() callers, bench.py host_fed).  Plain streams share the runtime's
+ * GPU_MAX_HW_QUEUES hardware queues (4 by default) round-robin, so a copy stream can land on
+ * the queue of an extraction stream and serialise behind it; this stream is created with a CU
+ * mask naming every CU of the device (hipExtStreamCreateWithCUMask), which the runtime serves
+ * from a queue of its own whatever GPU_MAX_HW_QUEUES says.  Non-blocking w.r.t. the null stream
+ * is NOT implied (order it with events).  orb_stream_destroy releases it (and the matcher scratch
+ * kept for it).  No reference counterpart (resource hook). */
+int orb_stream_create_dedicated(void** out_stream);
+int orb_stream_destroy(void* stream);
 
 /* ---- the rest of the ORBmatcher family (GPU: csrc/orb_match.hip) ------------------- */
 /* All entry points below take HOST buffers, run on the device of `device`, and are
@@ -227,6 +238,25 @@ int orb_search_by_bow_kf_f(const orb_frame_view_t* KF, const uint8_t* kf_usable,
 int orb_search_by_bow_kf_kf(const orb_frame_view_t* KF1, const uint8_t* usable1, orb_feature_vector_t fv1,
                             const orb_frame_view_t* KF2, const uint8_t* usable2, orb_feature_vector_t fv2,
                             float nnratio, int check_ori, int32_t* match12, int* n_matches, int device);
+
+/* SearchByBoW over many pairs per launch, on device-resident extractor output
+ * (orb_extract_batch_device: d_kps / d_desc [B][cap], d_counts[B]) and the FeatureVectors of the
+ * same frames (orb_vocabulary_transform_batch_device: d_fv_nodes [B][cap], d_fv_offsets
+ * [B][cap + 1], d_fv_features [B][cap], d_fv_n [B]).  Pair p = frames (d_pair_a[p], d_pair_b[p]):
+ *   kf_kf = 0: SearchByBoW(KeyFrame* = frame a, Frame& = frame b, vpMapPointMatches)
+ *              (ORBmatcher.cc:155-284; Tracking.cc:927 with nnratio 0.7): d_match[p][j] = the
+ *              frame-a keypoint matched to frame-b keypoint j, or -1;
+ *   kf_kf = 1: SearchByBoW(KeyFrame* = a, KeyFrame* = b, vpMatches12) (ORBmatcher.cc:715-850;
+ *              LoopClosing.cc:278 with 0.75): d_match[p][i1] = idx2 in frame b, or -1.
+ * d_usable [B][cap]: the frame's keypoint has a MapPoint that is not bad (both sides for kf_kf =
+ * 1, the KF side for kf_kf = 0); NULL = every keypoint.  d_match rows are written whole (-1 past
+ * the count); d_nmatches[p] = the reference's return value.  cap <= 8192, d_desc 16-B aligned.
+ * Asynchronous on `stream`. */
+int orb_search_by_bow_batch_device(int kf_kf, const orb_keypoint_t* d_kps, const uint8_t* d_desc,
+                                   const int32_t* d_counts, int cap, const uint32_t* d_fv_nodes,
+                                   const int32_t* d_fv_offsets, const int32_t* d_fv_features, const int32_t* d_fv_n,
+                                   int P, const int32_t* d_pair_a, const int32_t* d_pair_b, const uint8_t* d_usable,
+                                   float nnratio, int check_ori, int32_t* d_match, int32_t* d_nmatches, void* stream);
 
 /* SearchForTriangulation(KF1, KF2, F12, ...) (ORBmatcher.cc:852-1014) with
  * CheckDistEpipolarLine (136-153).  has_mp1/has_mp2: GetMapPointMatches()[i] != NULL.

@@ -126,6 +126,10 @@ HIP_SIGNATURES = {
         [_vp, _vp, _vp, _i, _i, _vp, _vp, FrameBounds, _f, _i, _i, _vp, _vp, _vp, _vp],
     ),
     "orb_match_release_stream_scratch": (_i, [_vp]),
+    "orb_stream_create_dedicated": (_i, [ctypes.POINTER(_vp)]),
+    "orb_search_by_bow_batch_device": (_i, [_i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _f, _i, _vp,
+                                            _vp, _vp]),
+    "orb_stream_destroy": (_i, [_vp]),
     "orb_features_in_area": (_i, [_pv, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i]),
     "orb_frame_is_in_frustum": (_i, [_pv, MapPoints, _f, _vp, _vp, _vp, _vp, _vp, _i]),
     "orb_search_by_bow_kf_f": (_i, [_pv, _vp, FeatureVectorCSR, _pv, FeatureVectorCSR, _f, _i, _vp, _pi, _i]),

@@ -1,0 +1,244 @@
+// orb_bow.hip — MI355X (gfx950) batched SearchByBoW: many (KeyFrame, Frame) or (KeyFrame,
+// KeyFrame) pairs per launch over device-resident extractor output and the FeatureVectors
+// orb_vocabulary_transform_batch_device writes (the reference's per-frame
+// Frame::ComputeBoW -> ORBmatcher::SearchByBoW chain, Tracking.cc:927 / LoopClosing.cc:278).
+//
+// Reference loop (ORBmatcher.cc:155-284, 715-850): walk the two FeatureVectors' common vocabulary
+// nodes in ascending id order; inside a node, every usable KF feature (in FeatureVector order)
+// takes the Hamming best / second best of the node's other-side features not yet matched in this
+// call, is accepted by TH_LOW and the ratio test, and marks its target matched; then the three
+// dominant rotation-histogram bins are kept.  A target feature sits in exactly ONE node of its
+// FeatureVector, so the "already matched" state of a node is touched only by that node's own
+// queries: nodes are independent and run in parallel (one wave per node), the queries of a node
+// in the reference's order.  Only the rotation filter is per pair.
+//
+// One 256-thread workgroup per pair:
+//   1. each thread binary-searches KF node positions in the other vector's node list (LDS);
+//   2. wave w takes the common nodes w, w+4, ...: per query (wave-uniform) every lane scores the
+//      node's candidates it holds (<= 64 candidates: one per lane, descriptor in registers for
+//      the whole node; more: strided, reloaded), key = (distance << 16) | candidate position, and
+//      two wave-min reductions give the reference's bestDist1 / bestIdx (first minimum in
+//      candidate order) and bestDist2; an accepted query marks its target in LDS and writes the
+//      output; the histogram counts by LDS atomics;
+//   3. ComputeThreeMaxima (ORBmatcher.cc:1748-1789) and the removal pass (bins recomputed from
+//      the keypoint angles of the kept outputs).
+// Latency-bound by design (sequential queries per node); SURVEY §8d-style bytes per pair:
+// 32 B per feature of both frames + 4 B per output slot.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <string>
+
+#include "../../include/orb_abi.h"
+#include "orb_device.h"
+#include "orb_internal.h"
+
+namespace {
+
+constexpr int TH_LOW = 50, HISTO = 30;  // ORBmatcher.cc:40-42
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+
+__device__ __forceinline__ uint32_t wmin(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
+    return v;
+}
+
+__device__ __forceinline__ int rot_bin(float a1, float a2) {  // ORBmatcher.cc:230-236 / 799-805
+    float rot = a1 - a2;
+    if (rot < 0.0f) rot += 360.0f;
+    int bin = (int)roundf(rot * (1.0f / HISTO));
+    if (bin == HISTO) bin = 0;
+    return bin;
+}
+
+__device__ __forceinline__ int ham(const uint4& a0, const uint4& a1, const uint4& b0, const uint4& b1) {
+    return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+           __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+struct BowBatch {
+    const orb_keypoint_t* kps;  // [B][cap]
+    const uint8_t* desc;        // [B][cap][32]
+    const int32_t* counts;      // [B]
+    const uint32_t* fvNodes;    // [B][cap]
+    const int32_t* fvOff;       // [B][cap + 1]
+    const int32_t* fvFeat;      // [B][cap]
+    const int32_t* fvN;         // [B]
+    const int32_t* pairA;       // [P] KF (KF1) frame
+    const int32_t* pairB;       // [P] F (KF2) frame
+    const uint8_t* usable;      // [B][cap] or NULL (every feature has a usable MapPoint)
+    int32_t* match;             // [P][cap]
+    int32_t* nmatches;          // [P]
+    int cap, kfkf, checkOri;
+    float nnratio;
+};
+
+__global__ void __launch_bounds__(256) k_bow_pairs(BowBatch J) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ int s_hist[HISTO];
+    __shared__ int s_ind[3];
+    __shared__ int s_acc, s_rem;
+    const int p = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int cap = J.cap;
+    const int fa = J.pairA[p], fb = J.pairB[p];
+    const int nA = min(J.counts[fa], cap), nB = min(J.counts[fb], cap);
+    const int nodesA = min(J.fvN[fa], nA), nodesB = min(J.fvN[fb], nB);
+    const uint32_t* NA = J.fvNodes + (size_t)fa * cap;
+    const uint32_t* NB = J.fvNodes + (size_t)fb * cap;
+    const int32_t* OA = J.fvOff + (size_t)fa * (cap + 1);
+    const int32_t* OB = J.fvOff + (size_t)fb * (cap + 1);
+    const int32_t* FA = J.fvFeat + (size_t)fa * cap;
+    const int32_t* FB = J.fvFeat + (size_t)fb * cap;
+    const orb_keypoint_t* KA = J.kps + (size_t)fa * cap;
+    const orb_keypoint_t* KB = J.kps + (size_t)fb * cap;
+    const uint4* DA = (const uint4*)(J.desc + (size_t)fa * cap * 32);
+    const uint4* DB = (const uint4*)(J.desc + (size_t)fb * cap * 32);
+    const uint8_t* UA = J.usable ? J.usable + (size_t)fa * cap : nullptr;
+    const uint8_t* UB = J.usable ? J.usable + (size_t)fb * cap : nullptr;
+    int32_t* out = J.match + (size_t)p * cap;
+    const int nOut = J.kfkf ? nA : nB;  // vpMatches12 over KF1 / vpMapPointMatches over F
+    int* s_mb = (int*)smem;                   // [cap] KF node position -> other node position or -1
+    uint8_t* s_taken = smem + 4 * (size_t)cap;  // [cap] other-side features matched (or unusable)
+
+    for (int i = tid; i < cap; i += 256) out[i] = -1;
+    for (int i = tid; i < nB; i += 256) s_taken[i] = (J.kfkf && UB) ? (uint8_t)(UB[i] == 0) : (uint8_t)0;
+    for (int a = tid; a < nodesA; a += 256) {  // the merge walk's common nodes (lower_bound)
+        const uint32_t id = NA[a];
+        int lo = 0, hi = nodesB;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (NB[mid] < id)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        s_mb[a] = (lo < nodesB && NB[lo] == id) ? lo : -1;
+    }
+    if (tid < HISTO) s_hist[tid] = 0;
+    if (tid == 0) s_acc = 0, s_rem = 0;
+    __syncthreads();
+
+    int acc = 0;  // accepted by this wave (lane 0 counts)
+    for (int a = wave; a < nodesA; a += 4) {
+        const int b = s_mb[a];
+        if (b < 0) continue;
+        const int q0 = OA[a], q1 = OA[a + 1], c0 = OB[b], nc = OB[b + 1] - c0;
+        if (nc <= 0) continue;
+        const bool small = nc <= 64;
+        // <= 64 candidates: one per lane, descriptor held for the whole node
+        int myIdx = 0;
+        uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
+        if (small && lane < nc) {
+            myIdx = min((unsigned)FB[c0 + lane], (unsigned)(nB - 1));  // (clamped: never outside the frame)
+            m0 = DB[2 * (size_t)myIdx];
+            m1 = DB[2 * (size_t)myIdx + 1];
+        }
+        for (int q = q0; q < q1; ++q) {
+            const int idx1 = __builtin_amdgcn_readfirstlane(FA[q]);
+            if ((unsigned)idx1 >= (unsigned)nA) continue;  // (not a feature of the frame: never from transform)
+            if (UA && !UA[idx1]) continue;  // !pMP || pMP->isBad()
+            const uint4 d0 = DA[2 * (size_t)idx1], d1 = DA[2 * (size_t)idx1 + 1];
+            uint32_t k1 = NONE, k2 = NONE;  // this lane's two smallest keys
+            if (small) {
+                if (lane < nc && !s_taken[myIdx]) k1 = ((uint32_t)ham(d0, d1, m0, m1) << 16) | (uint32_t)lane;
+            } else {
+                for (int j = lane; j < nc; j += 64) {
+                    const int idx2 = FB[c0 + j];
+                    if ((unsigned)idx2 >= (unsigned)nB || s_taken[idx2]) continue;
+                    const uint32_t key =
+                        ((uint32_t)ham(d0, d1, DB[2 * (size_t)idx2], DB[2 * (size_t)idx2 + 1]) << 16) | (uint32_t)j;
+                    if (key < k1) {
+                        k2 = k1;
+                        k1 = key;
+                    } else if (key < k2) {
+                        k2 = key;
+                    }
+                }
+            }
+            const uint32_t b1 = wmin(k1);
+            if (b1 == NONE) continue;  // bestDist1 stays INT_MAX
+            const uint32_t b2 = wmin(k1 == b1 ? k2 : k1);
+            const int dist1 = (int)(b1 >> 16);
+            const int dist2 = b2 == NONE ? INT_MAX : (int)(b2 >> 16);
+            const bool thOk = J.kfkf ? dist1 < TH_LOW : dist1 <= TH_LOW;
+            if (!(thOk && (float)dist1 < J.nnratio * (float)dist2)) continue;
+            const int jb = (int)(b1 & 0xFFFFu);
+            const int idx2 = small ? __shfl(myIdx, jb, 64) : FB[c0 + jb];
+            if (lane == 0) {
+                s_taken[idx2] = 1;
+                if (J.kfkf)
+                    out[idx1] = idx2;  // vpMatches12[idx1] = vpMapPoints2[bestIdx2]
+                else
+                    out[idx2] = idx1;  // vpMapPointMatches[bestIdxF] = pMP (the KF feature)
+                if (J.checkOri) atomicAdd(&s_hist[rot_bin(KA[idx1].angle, KB[idx2].angle)], 1);
+                ++acc;
+            }
+            // lane 0's LDS write lands before any lane's next read (same wave, in order)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+    }
+    if (lane == 0 && acc) atomicAdd(&s_acc, acc);
+    __syncthreads();  // (also orders the output writes before the removal pass reads them)
+    if (J.checkOri) {
+        if (tid == 0) {  // ComputeThreeMaxima (ORBmatcher.cc:1748-1789)
+            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+            for (int i = 0; i < HISTO; ++i) {
+                const int sz = s_hist[i];
+                if (sz > max1) {
+                    max3 = max2, max2 = max1, max1 = sz;
+                    ind3 = ind2, ind2 = ind1, ind1 = i;
+                } else if (sz > max2) {
+                    max3 = max2, max2 = sz;
+                    ind3 = ind2, ind2 = i;
+                } else if (sz > max3) {
+                    max3 = sz, ind3 = i;
+                }
+            }
+            if (max2 < 0.1f * (float)max1) {
+                ind2 = -1, ind3 = -1;
+            } else if (max3 < 0.1f * (float)max1) {
+                ind3 = -1;
+            }
+            s_ind[0] = ind1, s_ind[1] = ind2, s_ind[2] = ind3;
+        }
+        __syncthreads();
+        int rem = 0;
+        for (int i = tid; i < nOut; i += 256) {
+            const int v = out[i];
+            if (v < 0) continue;
+            const int bin = J.kfkf ? rot_bin(KA[i].angle, KB[v].angle) : rot_bin(KA[v].angle, KB[i].angle);
+            if (bin != s_ind[0] && bin != s_ind[1] && bin != s_ind[2]) {
+                out[i] = -1;
+                ++rem;
+            }
+        }
+        if (rem) atomicAdd(&s_rem, rem);
+        __syncthreads();
+    }
+    if (tid == 0) J.nmatches[p] = s_acc - s_rem;
+}
+
+}  // namespace
+
+extern "C" int orb_search_by_bow_batch_device(int kf_kf, const orb_keypoint_t* d_kps, const uint8_t* d_desc,
+                                              const int32_t* d_counts, int cap, const uint32_t* d_fv_nodes,
+                                              const int32_t* d_fv_offsets, const int32_t* d_fv_features,
+                                              const int32_t* d_fv_n, int P, const int32_t* d_pair_a,
+                                              const int32_t* d_pair_b, const uint8_t* d_usable, float nnratio,
+                                              int check_ori, int32_t* d_match, int32_t* d_nmatches, void* stream) {
+    if (P < 0 || cap <= 0 || cap > 8192 || (kf_kf != 0 && kf_kf != 1))
+        return orb_internal_set_error(ORB_EINVAL, "bad arguments");
+    if (P == 0) return ORB_OK;
+    if (!d_kps || !d_desc || !d_counts || !d_fv_nodes || !d_fv_offsets || !d_fv_features || !d_fv_n || !d_pair_a ||
+        !d_pair_b || !d_match || !d_nmatches)
+        return orb_internal_set_error(ORB_EINVAL, "bad arguments");
+    if (((uintptr_t)d_desc & 15) != 0) return orb_internal_set_error(ORB_EINVAL, "descriptors must be 16-B aligned");
+    BowBatch J{d_kps, d_desc, d_counts, d_fv_nodes, d_fv_offsets, d_fv_features, d_fv_n, d_pair_a, d_pair_b,
+               d_usable, d_match, d_nmatches, cap, kf_kf, check_ori ? 1 : 0, nnratio};
+    const size_t lds = 5 * (size_t)cap;
+    hipLaunchKernelGGL(k_bow_pairs, dim3(P), dim3(256), lds, (hipStream_t)stream, J);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return orb_internal_set_error(ORB_EDEVICE, std::string("k_bow_pairs: ") + hipGetErrorString(e));
+    return ORB_OK;
+}

@@ -1676,23 +1676,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
 //       ((S-1) << 24) | (y << 12) | x (k_select restores raster order).
 // The 7x7 blur of the descriptors is not materialised: k_orient_desc evaluates it at the
 // rBRIEF sample points from a raw window (ORBextractor.cc:760).
-#ifndef FT_TW_MAX
 #define FT_TW_MAX 256     // detection columns per tile at most (64 lanes x 4 pixels)
-#endif
-#ifndef FT_IN_BYTES
 #define FT_IN_BYTES 12672  // staged-tile LDS budget (44 rows of 288 B at TW = 256)
-#endif
-#ifndef FT_S_BYTES
 #define FT_S_BYTES 10032   // strength-plane LDS budget (38 rows of 264 B at TW = 256; a multiple of 16)
-#endif
 static_assert(FT_S_BYTES % 16 == 0 && FT_IN_BYTES % 16 == 0, "k_fast's LDS buffers are cleared / staged in 16-B units");
-#ifndef FT_Q
 #define FT_Q 512           // per-wave queue (u16 entries): dwords, then the NMS corner list
-#endif
 #define FT_CQ 320          // per-wave pixel list (u16 entries): < 64 carried + 256 expanded
 #ifndef FT_CL
 #define FT_CL 256          // per-wave corner list (u16 entries) filled by the strength passes; a
                            // workgroup where a wave has more corners scans the strength plane instead
+                           // (a test build with -DFT_CL=8 forces that fallback: tests/test_gpu_fast_fallback.py)
 #endif
 struct FastTile {
     int level, x0, y0;  // detection origin (level coordinates); x0 = 16 + k TW, a multiple of 4
@@ -1703,22 +1696,10 @@ struct FastTile {
     uint32_t rcpU;      // ceil(2^32 / (sp / 16)): staged unit -> row
 };
 
-#ifndef KF_XCD
-#define KF_XCD 0  // 1: XCD-aware workgroup order; measured slower (0.646 vs 0.574 ms c3, 0.913
-                  // vs 0.832 c4, 1.627 vs 1.557 720p): the halo re-reads are not what binds
-#endif
 #ifndef KF_DPL
 #define KF_DPL 2  // adjacent dwords per lane and step of the compass loop (1, 2 or 4)
 #endif
-#ifndef KF_WAVES
-#define KF_WAVES 0  // > 0: waves per SIMD the register allocation targets
-#endif
-#if KF_WAVES
-#define KF_ATTR __attribute__((amdgpu_waves_per_eu(KF_WAVES)))
-#else
-#define KF_ATTR
-#endif
-__global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict__ pyr, Geom g,
+__global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, Geom g,
                                                       const FastTile* __restrict__ tiles,
                                                       uint32_t* __restrict__ cand, int* __restrict__ cellCount) {
     __shared__ __attribute__((aligned(16))) uint8_t s_in[FT_IN_BYTES];
@@ -1732,19 +1713,10 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
     __shared__ uint8_t s_cm[FT_TW_MAX / 4 + 2 + KF_DPL];  // per flattened dword column: its detection
                                                            // pixels (0 past the ring)
     KF_T(0);
-#if KF_XCD
-    // XCD-aware order: workgroup i runs on XCD i % 8, so give each XCD a contiguous run of
-    // (frame, tile) ids — consecutive tiles are vertically adjacent in one column strip, and
-    // their shared halo rows then hit in that XCD's L2
-    int bid = blockIdx.y * gridDim.x + blockIdx.x;
-    const int full = (gridDim.x * gridDim.y) & ~7;
-    if (bid < full) bid = (bid & 7) * (full >> 3) + (bid >> 3);
-    const int b = (int)((uint32_t)bid / gridDim.x);
-    FastTile t = tiles[bid - b * (int)gridDim.x];
-#else
+    // (plain block order: an XCD-aware order, vertically adjacent tiles on one XCD so their halo
+    // rows hit in its L2, measured slower -- 0.646 vs 0.574 ms c3: the halo is not what binds)
     FastTile t = tiles[blockIdx.x];
     const int b = blockIdx.y;
-#endif
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     // the level's geometry and the tile in SGPRs for the whole kernel (read through a reference
     // into the kernarg block, the compiler re-issued dependent s_loads inside the loops); the
@@ -2050,9 +2022,6 @@ __global__ void __launch_bounds__(256) KF_ATTR k_fast(const uint8_t* __restrict_
 // OD_WAVES keypoint slots per workgroup.  A wave's window and sums are its own (LDS is in order
 // per wave); the two workgroup barriers only hand the IC moments to wave 0, which computes the
 // slots' angle / sin / cos once, and hand those back.
-#ifndef OD_XCD  // 0: plain block order (experiments)
-#define OD_XCD 1
-#endif
 #define OD_WR 21   // window reach: rBRIEF |offset| <= 18 + the blur's 3
 #ifndef OD_WP
 #define OD_WP 64   // LDS row pitch of the raw window (bytes).  80 (row blocks 4 rows apart on
@@ -2147,7 +2116,7 @@ __global__ void __launch_bounds__(64 * OD_WAVES) k_orient_desc(const uint8_t* __
     // of keypoints (neighbouring keypoints share window rows: L2 hits instead of HBM re-reads)
     int bid = blockIdx.y * gridDim.x + blockIdx.x;
     const int full = (gridDim.x * gridDim.y) & ~7;
-    if (OD_XCD && bid < full) bid = (bid & 7) * (full >> 3) + (bid >> 3);
+    if (bid < full) bid = (bid & 7) * (full >> 3) + (bid >> 3);
     const int b = (int)__umulhi((uint32_t)bid, g.odDivMagic);  // bid / gridDim.x (exact: bid * gridDim.x < 2^32)
     const int k = (bid - b * gridDim.x) * OD_WAVES + wave;  // slot: level l owns [kpBase_l, kpBase_l + nDesired_l)
     // wave-uniform record: x, y and the window base live in SGPRs (its load first: the window's
@@ -4182,6 +4151,29 @@ int orb_match_release_stream_scratch(void* stream) {
             g_big.erase(g_big.begin() + (long)i);
             return ORB_OK;
         }
+    return ORB_OK;
+}
+
+// A stream with every CU in its mask: the runtime gives a CU-masked stream a hardware queue of
+// its own instead of sharing one of its GPU_MAX_HW_QUEUES round-robin (include/orb_abi.h).
+int orb_stream_create_dedicated(void** out_stream) {
+    if (!out_stream) return set_err(ORB_EINVAL, "bad arguments");
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    int ncu = 0;
+    HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0xFFFFFFFFu);
+    if (ncu % 32) mask.back() = (1u << (ncu % 32)) - 1u;
+    hipStream_t st = nullptr;
+    HIP_TRY(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
+    *out_stream = (void*)st;
+    return ORB_OK;
+}
+
+int orb_stream_destroy(void* stream) {
+    if (!stream) return set_err(ORB_EINVAL, "bad arguments");
+    orb_match_release_stream_scratch(stream);
+    HIP_TRY(hipStreamDestroy((hipStream_t)stream));
     return ORB_OK;
 }
 

@@ -279,3 +279,30 @@ class ORBmatcher:
             bounds if bounds is not None else FrameBounds(0, width, 0, height), self.mfNNratio, int(self.mbCheckOrientation), int(windowSize),
             ptr(d_prev_xy), ptr(m12), ptr(nm), ctypes.c_void_p(s.cuda_stream)))
         return m12, nm
+
+    def search_by_bow_batch_device(self, kf_kf: bool, d_kps, d_desc, d_counts, fv: dict, pair_a, pair_b,
+                                   d_usable=None, stream=None):
+        """SearchByBoW over many pairs in one launch (orb_search_by_bow_batch_device).
+
+        d_kps (B, cap, 28) / d_desc (B, cap, 32) / d_counts (B,) as ORBextractor.extract_batch_device
+        returns them; `fv` = ORBVocabulary.transform_batch_device's dict for the same frames;
+        pair_a / pair_b int32 device tensors (P,): the KeyFrame (KF1) and the Frame (KF2) of each
+        pair.  kf_kf False: SearchByBoW(KeyFrame*, Frame&) (ORBmatcher.cc:155-284), row p of the
+        result = vpMapPointMatches over frame b's keypoints (frame-a keypoint index or -1); True:
+        SearchByBoW(KeyFrame*, KeyFrame*) (715-850), row p = vpMatches12 over frame a's keypoints.
+        d_usable (B, cap) uint8 or None (every keypoint has a usable MapPoint).
+        Returns (d_match (P, cap) int32, d_nmatches (P,) int32).
+        """
+        import torch
+
+        P = int(pair_a.shape[0])
+        cap = int(d_kps.shape[1])
+        dev = d_kps.device
+        m = torch.empty((P, cap), dtype=torch.int32, device=dev)
+        n = torch.empty((P,), dtype=torch.int32, device=dev)
+        s = stream if stream is not None else torch.cuda.current_stream(dev)
+        check(self._lib.orb_search_by_bow_batch_device(
+            int(bool(kf_kf)), ptr(d_kps), ptr(d_desc), ptr(d_counts), cap, ptr(fv["fv_nodes"]), ptr(fv["fv_offsets"]),
+            ptr(fv["fv_features"]), ptr(fv["fv_n"]), P, ptr(pair_a), ptr(pair_b), ptr(d_usable), self.mfNNratio,
+            int(self.mbCheckOrientation), ptr(m), ptr(n), ctypes.c_void_p(s.cuda_stream)))
+        return m, n

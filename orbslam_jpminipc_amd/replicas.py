@@ -3,8 +3,9 @@
 Frames of different streams are independent and SearchForInitialization pairs frames of
 the same stream, so the front end shards as replicas: stream s runs on
 rank s mod world.  The only cross-rank traffic is the benchmark's barrier and the max over
-ranks of the timed region (a 1-element all-reduce), on the "nccl" (RCCL) backend on GPUs or
-"gloo" on CPU.
+ranks of the timed region (a 1-element all-reduce) and a gather of the per-rank seconds.  These
+scalars go over "gloo" by default, on GPUs too: nothing on the data path is exchanged, so
+RCCL ("nccl") would add only its per-rank init; it stays selectable.
 """
 from __future__ import annotations
 
@@ -29,7 +30,7 @@ def init_from_env(backend: str | None = None) -> DistInfo:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and not dist.is_initialized():
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            backend = "gloo"
         if backend == "nccl":
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))

@@ -3,6 +3,7 @@
 product sources are never modified): ablation_variant.py NAME 'old1' 'new1' ['old2' 'new2' ...]
 applies exact-string replacements to orb_hip.hip in a scratch copy and builds
 build/variants/NAME.so.  Wrong-output ablations live only in these scratch builds."""
+import os
 import pathlib
 import shutil
 import subprocess
@@ -25,13 +26,24 @@ for f in (tmp / "csrc").glob("*.hip"):
     t = f.read_text().replace('"../../include/orb_abi.h"', '"../include/orb_abi.h"')
     f.write_text(t)
 units = [tmp / "csrc" / u for u in ("orb_hip.hip", "orb_match.hip", "orb_voc.hip", "orb_mappoint.hip",
-                                    "orb_pipeline.hip", "orb_persist.hip", "orb_frame.hip")]
+                                    "orb_pipeline.hip", "orb_persist.hip", "orb_frame.hip", "orb_bow.hip")]
 out = ROOT / "build" / "variants" / f"{name}.so"
 out.parent.mkdir(parents=True, exist_ok=True)
 sys.path.insert(0, str(ROOT))
 from __graft_entry__ import hipcc_flags  # noqa: E402  (the library's flags, optional ones probed)
 
 flags = hipcc_flags()
+if os.environ.get("ORB_VARIANT_NO_OPT"):  # without the probed OPTIONAL_FLAGS (-amdgpu-mfma-vgpr-form=1)
+    from __graft_entry__ import HIPCC_FLAGS  # noqa: E402
+    flags = list(HIPCC_FLAGS)
+flags = flags + os.environ.get("ORB_VARIANT_EXTRA", "").split()
+if os.environ.get("ORB_VARIANT_ASM"):  # device assembly of orb_hip.hip only: build/variants/NAME.s
+    flags = [f for f in flags if f not in ("-shared", "-fPIC")] + os.environ.get("ORB_VARIANT_FLAGS", "").split()
+    out = out.with_suffix(".s")
+    r = subprocess.run(["/opt/rocm/bin/hipcc", *flags, "--cuda-device-only", "-S", "-o", str(out), str(units[0])],
+                       capture_output=True, text=True)
+    shutil.rmtree(tmp)
+    sys.exit(r.stderr[-3000:] if r.returncode else print("asm", out))
 r = subprocess.run(["/opt/rocm/bin/hipcc", *flags, "-o", str(out), *map(str, units)], capture_output=True, text=True)
 shutil.rmtree(tmp)
 if r.returncode:

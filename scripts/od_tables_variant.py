@@ -26,6 +26,26 @@ reps = [
   "    int st = upload_pattern(device);\n    ODTables odt{};\n    HIP_TRY(hipGetSymbolAddress((void**)&odt.rowB, HIP_SYMBOL(c_rowB)));\n    HIP_TRY(hipGetSymbolAddress((void**)&odt.icmask, HIP_SYMBOL(c_icmask)));\n    HIP_TRY(hipGetSymbolAddress((void**)&odt.patf, HIP_SYMBOL(c_patternf)));\n"),
  ("    orb_extractor* h = new orb_extractor();\n", "    orb_extractor* h = new orb_extractor();\n    h->odTables = odt;\n"),
 ]
+if len(sys.argv) > 2 and sys.argv[2] == "nop":  # + 64 wait states between the row pass and the pattern loads
+    reps.append(("    float pat[16];  // pattern points",
+                 "    __builtin_amdgcn_sched_barrier(0);\n    asm volatile(\"s_nop 7\\n\\ts_nop 7\\n\\ts_nop 7\\n\\ts_nop 7\\n\\ts_nop 7\\n\\ts_nop 7\\n\\ts_nop 7\\n\\ts_nop 7\" ::: \"memory\");\n    __builtin_amdgcn_sched_barrier(0);\n    float pat[16];  // pattern points"))
+LOADLINE = "        const f32x4v f = OD_LD(f32x4v, patf, 16u * (4u * (uint32_t)lane + q));"
+mode = sys.argv[2] if len(sys.argv) > 2 else ""
+if mode in ("sc", "asmwait"):  # the pattern loads as asm (sc: with sc0 sc1, no L1 / TCP hit), waited inside it
+    reps[4] = (reps[4][0], reps[4][1].replace(LOADLINE,
+        "        f32x4v f;\n        asm volatile(\"global_load_dwordx4 %0, %1, %2" + (" sc0 sc1" if mode == "sc" else "") + "\\n\\ts_waitcnt vmcnt(0)\" : \"=v\"(f) : \"v\"(16u * (4u * (uint32_t)lane + q)), \"s\"(tb.patf) : \"memory\");"))
+elif mode == "dw":  # four dword loads per float4 instead of one dwordx4 (asm: not re-merged), waited in the asm
+    reps[4] = (reps[4][0], reps[4][1].replace(LOADLINE,
+        "        f32x4v f;\n        asm volatile(\"global_load_dword %0, %4, %5\\n\\tglobal_load_dword %1, %4, %5 offset:4\\n\\t"
+        "global_load_dword %2, %4, %5 offset:8\\n\\tglobal_load_dword %3, %4, %5 offset:12\\n\\ts_waitcnt vmcnt(0)\" "
+        ": \"=&v\"(f.x), \"=&v\"(f.y), \"=&v\"(f.z), \"=&v\"(f.w) : \"v\"(16u * (4u * (uint32_t)lane + q)), \"s\"(tb.patf) : \"memory\");"))
+elif mode == "malloc":  # the pattern copied to a hipMalloc buffer (not the code object's segment)
+    reps[7] = (reps[7][0], reps[7][1] + "    { void* pm = nullptr; HIP_TRY(hipMalloc(&pm, 4096)); HIP_TRY(hipMemcpy(pm, odt.patf, 4096, hipMemcpyDeviceToDevice)); odt.patf = (const float4*)pm; }\n")
+elif mode == "drainexit":  # E1: waves without a keypoint drain their loads before they end
+    reps.append(("    if (!active) return;", "    if (!active) {\n        asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n        return;\n    }"))
+elif mode == "prewait":  # E2: compiler-placed pattern loads, every wave waits for them before the barrier
+    reps.append(("    lds_barrier();  // s_trig is written", "    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n    lds_barrier();  // s_trig is written"))
+assert LOADLINE in reps[4][1] or mode in ("sc", "asmwait", "dw")
 args = ["python3", "scripts/ablation_variant.py", sys.argv[1]]
 for a, b in reps:
     args += [a, b]

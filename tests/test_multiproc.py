@@ -31,7 +31,10 @@ def _worker(rank, world, port, q):
     from orbslam_jpminipc_amd import replicas
     from oracle_lib import Oracle
 
-    info = replicas.init_from_env("gloo")
+    info = replicas.init_from_env()  # the default control plane (gloo), as bench.py --gpus N uses
+    import torch.distributed as dist
+
+    assert dist.get_backend() == "gloo"
     streams = replicas.streams_of_rank(4, info.rank, info.world)
     ora = Oracle(300, 1.2, 4, 1, 20)
     replicas.barrier(info)
