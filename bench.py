@@ -37,6 +37,10 @@ Also reported:
                 boundary: ORBextractor.h:43-45), H2D / compute / D2H overlapped on three streams;
                 frames/s with the PCIe GB/s achieved each way and the link's measured ceiling
                 (rank 0, N = 1; never `value`)
+  bow           the BoW-bucketed matching path on the step's output: vocabulary transform
+                (Frame::ComputeBoW, levelsup 4, ORBvoc-shaped tree) of every frame + batched
+                SearchByBoW(KF = frame t, F = frame t+1), per-stage ms, pairs/s, rooflines (rank 0,
+                N = 1; never `value`)
   cpu_baseline  the CPU oracle (C++ restatement, oracle/) on the host cores, rank 0, N = 1, on a
                 bounded sample of the same frames: extract-only and extract+match frames/s on all
                 threads and on the cgroup quota's thread count (value = the better of the two,
@@ -368,6 +372,83 @@ def latency_b1(orb, W, H, NF, device, frames, reps=100):
                 "the FAST(7) re-runs always run in k_rerun (more workgroups per (frame, level) at small "
                 "batches), and batches below 256 frames build the pyramid with per-level launches "
                 "(k_pyr0, k_pyr_resize)",
+    }
+
+
+def orbvoc_shaped_tree(k=10, L=6, seed=106):
+    """An ORBvoc.txt-shaped vocabulary (k = 10, L = 6: 1 111 111 nodes, TF-IDF, L1) in file order,
+    random node descriptors and leaf weights: the reference ships no vocabulary (Data/ is not in
+    the repository) and nothing can be downloaded here."""
+    rng = np.random.default_rng(seed)
+    n = sum(k ** d for d in range(1, L + 1))
+    parent = np.zeros(n, np.int32)
+    width, pos, prev_first = 1, 0, 0
+    for _ in range(1, L + 1):
+        parent[pos:pos + width * k] = np.repeat(np.arange(prev_first, prev_first + width, dtype=np.int32), k)
+        prev_first = pos + 1
+        pos += width * k
+        width *= k
+    leaf = np.zeros(n, np.uint8)
+    leaf[n - k ** L:] = 1
+    desc = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    weight = np.where(leaf > 0, rng.uniform(0.0, 3.0, size=n), 0.0)
+    return parent, leaf, desc, weight
+
+
+def bow_leg(orb, d_kps, d_desc, d_cnt, f1, f2, steps, warmup, stream):
+    """The BoW-bucketed matching path on the step's extractor output (north_star: "BoW-bucketed
+    matching"): Frame::ComputeBoW for every frame (TemplatedVocabulary::transform with levelsup 4,
+    Frame.cc:280-287) then SearchByBoW(KeyFrame = frame t, Frame = frame t+1) with
+    TrackReferenceKeyFrame's ORBmatcher(0.7, true) (Tracking.cc:927), every KF keypoint taken as
+    holding a good MapPoint (the most work per pair).  Both batched on the device, one stream;
+    each stage timed with HIP events on that stream."""
+    import torch
+
+    voc = orb.ORBVocabulary.from_arrays(10, 6, 0, 0, *orbvoc_shaped_tree())
+    matcher = orb.ORBmatcher(0.7, True)
+    B, cap = int(d_desc.shape[0]), int(d_desc.shape[1])
+    with torch.cuda.stream(stream):
+        fv = voc.transform_batch_device(d_desc, d_cnt, 4, stream=stream)
+        for _ in range(warmup):
+            voc.transform_batch_device(d_desc, d_cnt, 4, out=fv, stream=stream)
+            m, nm = matcher.search_by_bow_batch_device(False, d_kps, d_desc, d_cnt, fv, f1, f2, stream=stream)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        t_tr = t_m = 0.0
+        for _ in range(steps):
+            ev[0].record(stream)
+            voc.transform_batch_device(d_desc, d_cnt, 4, out=fv, stream=stream)
+            ev[1].record(stream)
+            m, nm = matcher.search_by_bow_batch_device(False, d_kps, d_desc, d_cnt, fv, f1, f2, stream=stream)
+            ev[2].record(stream)
+            ev[2].synchronize()
+            t_tr += ev[0].elapsed_time(ev[1])
+            t_m += ev[1].elapsed_time(ev[2])
+    t_tr /= steps
+    t_m /= steps
+    cnt = d_cnt.cpu().numpy().astype(np.int64)
+    nm_h = nm.cpu().numpy()
+    P = int(f1.numel())
+    nfeat = int(cnt.sum())
+    f1h, f2h = f1.cpu().numpy(), f2.cpu().numpy()
+    # algorithmic bytes: transform = every descriptor read once + its BowVector / FeatureVector
+    # entries written (word u32, weight f64, node u32, BowVector word + value, FeatureVector node /
+    # offset / feature: 40 B per feature) -- the tree itself is cache-resident reuse, not counted;
+    # match = both frames' descriptors read once + the output row (4 B per slot of frame b)
+    b_tr = nfeat * (32 + 40)
+    b_m = int(sum(32 * (cnt[a] + cnt[b]) + 4 * cap for a, b in zip(f1h, f2h)))
+    return {
+        "what": "Frame::ComputeBoW (transform, levelsup 4) on every frame + SearchByBoW(KF = frame t, F = frame t+1), "
+                "ORBmatcher(0.7, true), batched on the device",
+        "vocabulary": "ORBvoc-shaped random tree: k=10, L=6, 1111111 nodes, TF-IDF / L1 (no ORBvoc.txt in the reference)",
+        "frames": B, "pairs": P, "features": nfeat,
+        "transform_ms": t_tr, "match_ms": t_m, "ms_per_step": t_tr + t_m,
+        "frames_per_s": B / ((t_tr + t_m) * 1e-3), "pairs_per_s": P / (t_m * 1e-3),
+        "matches_per_pair": float(nm_h.mean()),
+        "transform_roofline": {"bound": "hbm", "achieved": b_tr / (t_tr * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                               "unit": "GB/s", "frac": b_tr / (t_tr * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                               "algorithmic_bytes": b_tr},
+        "match_roofline": {"bound": "hbm", "achieved": b_m / (t_m * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": b_m / (t_m * 1e-3) / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes": b_m},
     }
 
 
@@ -816,6 +897,8 @@ def run_rank(args):
         hf = host_fed(ext, matcher, frames, f1, f2, W, H, 10, 8)
         hf["vs_device_resident"] = hf["value"] / value
         result["host_fed"] = hf
+    if rank == 0 and world == 1 and args.bow:
+        result["bow"] = bow_leg(orb, d_kps, d_desc, d_cnt, f1, f2, 10, 3, s_ext)
     if rank == 0 and world == 1 and args.latency:
         result["latency_b1"] = latency_b1(orb, W, H, NF, local, frames[:2])
     if rank == 0 and world == 1 and args.cpu_frames > 0:
@@ -896,6 +979,8 @@ def main():
     ap.add_argument("--latency", type=int, default=1, help="1: measure latency_b1 (rank 0, N = 1)")
     ap.add_argument("--host-fed", type=int, default=1,
                     help="1: measure the host-fed step (pinned host frames in, host results out; rank 0, N = 1)")
+    ap.add_argument("--bow", type=int, default=1,
+                    help="1: measure the BoW leg (vocabulary transform + batched SearchByBoW; rank 0, N = 1)")
     ap.add_argument("--overlap", type=int, default=0,
                     help="0 (default): serial step; 1 / 2: stream-overlap experiments, measured slower")
     ap.add_argument("--survey-steps", type=int, default=5, help="untimed steps with every stage bracketed")

@@ -518,6 +518,11 @@ int orb_debug_cell_counts(orb_extractor_t* h, int b, int l, int* counts, int cap
  * otherwise), 1 = per-level launches always, 2 = k_pyr_stream at every batch size of grey
  * frames whenever the current geometry has a stream plan. */
 int orb_debug_set_pyramid_path(orb_extractor_t* h, int mode);
+/* k_fast keeps each wave's corners in a list of up to 256 entries and falls back to scanning the
+ * whole strength plane of its tile when a wave finds more; cap (0 .. 256) lowers that list's
+ * capacity for the next extractions so the fallback runs on ordinary frames (results are
+ * identical; test hook, tests/test_gpu_fast_fallback.py).  The default is 256. */
+int orb_debug_set_fast_corner_list(orb_extractor_t* h, int cap);
 /* The current geometry's k_pyr_stream plan: returns 1 (and level-0 rows per round, rounds,
  * LDS bytes) when there is one, 0 when the geometry only runs per-level launches. */
 int orb_debug_pyramid_plan(const orb_extractor_t* h, int* rows_per_round, int* rounds, int* lds_bytes);

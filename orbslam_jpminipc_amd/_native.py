@@ -127,6 +127,7 @@ HIP_SIGNATURES = {
     ),
     "orb_match_release_stream_scratch": (_i, [_vp]),
     "orb_stream_create_dedicated": (_i, [ctypes.POINTER(_vp)]),
+    "orb_debug_set_fast_corner_list": (_i, [_vp, _i]),
     "orb_search_by_bow_batch_device": (_i, [_i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _f, _i, _vp,
                                             _vp, _vp]),
     "orb_stream_destroy": (_i, [_vp]),
@@ -232,7 +233,12 @@ def hip_lib() -> ctypes.CDLL:
         except OSError as e:  # pragma: no cover - environment dependent
             raise NativeLibraryError(f"cannot load {HIP_LIB_PATH}: {e}") from e
         for name, (res, args) in HIP_SIGNATURES.items():
-            fn = getattr(lib, name)
+            try:
+                fn = getattr(lib, name)
+            except AttributeError:
+                if os.environ.get("ORB_HIP_LIB"):  # an experiment build of an older ABI
+                    continue
+                raise
             fn.restype = res
             fn.argtypes = args
         _hip = lib

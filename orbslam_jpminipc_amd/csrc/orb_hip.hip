@@ -130,6 +130,8 @@ struct Geom {
     int umax[16];
     unsigned long long umaxNib;  // umax[0..15] as 4-bit nibbles (k_orient_desc's disc mask)
     uint32_t odDivMagic;          // k_orient_desc: ceil(2^32 / slot groups per frame) (exact division)
+    int fastCl;                   // k_fast: per-wave corner-list capacity used (FT_CL; smaller only via
+                                  // orb_debug_set_fast_corner_list, to exercise the plane-scan fallback)
     LevelGeom lv[ORB_MAX_LEVELS];
 };
 
@@ -1084,8 +1086,8 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
     // test s0 - 1 > (n > t ? n - 1 : 0) reads the plane as is (out-of-cell neighbours 0).  Each
     // wave scans its share of the plane's dwords, ballot-compacts the nonzero pixels into its
     // queue (the strength pass is done with it) and runs the NMS one corner per lane, all nine
-    // reads issued together; a survivor sets its bit, counts into its row (LDS atomics) and
-    // appends its record to the list
+    // reads issued together; a survivor sets its bit in its row's mask and counts into its row
+    // (LDS atomics); the per-word pass below turns the masks into raster-order records
     {
         uint32_t* q = (uint32_t*)(In + inW * (dh + 6)) + 4 + wave * (RR_Q + 8);
         const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -1682,11 +1684,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
 static_assert(FT_S_BYTES % 16 == 0 && FT_IN_BYTES % 16 == 0, "k_fast's LDS buffers are cleared / staged in 16-B units");
 #define FT_Q 512           // per-wave queue (u16 entries): dwords, then the NMS corner list
 #define FT_CQ 320          // per-wave pixel list (u16 entries): < 64 carried + 256 expanded
-#ifndef FT_CL
 #define FT_CL 256          // per-wave corner list (u16 entries) filled by the strength passes; a
                            // workgroup where a wave has more corners scans the strength plane instead
-                           // (a test build with -DFT_CL=8 forces that fallback: tests/test_gpu_fast_fallback.py)
-#endif
+                           // (Geom::fastCl lowers the cap for the fallback's parity test)
 struct FastTile {
     int level, x0, y0;  // detection origin (level coordinates); x0 = 16 + k TW, a multiple of 4
     int tw4, th;        // dwords per row (>= 2), rows (clipped to the detection region)
@@ -1795,7 +1795,7 @@ __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, G
         const uint64_t m = __ballot(corner);
         if (corner) {
             const int ix = ncl + __popcll(m & below);
-            cl[ix < FT_CL ? ix : FT_CL] = code;  // FT_CL: trash slot
+            cl[ix < g.fastCl ? ix : FT_CL] = code;  // FT_CL: trash slot
         }
         ncl += __popcll(m);
     };
@@ -1892,7 +1892,7 @@ __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, G
         drain(qn);
         if (np) strength_pass(0, np);  // the remainder, < 64 pixels
     }
-    if (ncl > FT_CL && lane == 0) s_ovf = 1;
+    if (ncl > g.fastCl && lane == 0) s_ovf = 1;
     KF_T(3);
     __syncthreads();
     KF_T(4);
@@ -2921,6 +2921,7 @@ struct orb_extractor {
     // geometry of the current frame size
     int W = 0, H = 0;
     Geom g{};
+    int fastCl = FT_CL;  // orb_debug_set_fast_corner_list
     std::vector<CellGeom> cells;
     std::vector<int> rtab;
     size_t listLds = 0;  // k_select<.., false> (re-runs in k_rerun): the survivor lists only
@@ -3081,6 +3082,7 @@ struct orb_extractor {
         Geom G{};
         G.L = nlevels;
         G.fastTh = std::min(std::max(fastTh, 0), 255);
+        G.fastCl = fastCl;
         G.scoreType = scoreType;
         int k7[7];
         gaussian_taps7(k7);
@@ -4289,6 +4291,13 @@ int orb_debug_set_pyramid_path(orb_extractor_t* h, int mode) {
     if (!h || mode < 0 || mode > 2) return set_err(ORB_EINVAL, "mode must be 0, 1 or 2");
     h->pyrLegacy = mode == 1;
     h->pyrStreamAlways = mode == 2;
+    return ORB_OK;
+}
+
+int orb_debug_set_fast_corner_list(orb_extractor_t* h, int cap) {
+    if (!h || cap < 0 || cap > FT_CL) return set_err(ORB_EINVAL, "cap must be in [0, 256]");
+    h->fastCl = cap;
+    h->g.fastCl = cap;
     return ORB_OK;
 }
 

@@ -23,6 +23,20 @@ tot = 0
 for fi, img in enumerate(orb.synth_stream(W, H, stream=3, first=0, count=3)):
     for rep in range(REPS):
         kg, dg = ext(img)
+        if hasattr(orb.hip_lib(), "orb_variant_odp"):  # probe builds: pattern registers that differ
+            import ctypes
+
+            buf = np.zeros(8 * 512, np.uint32)
+            fn = orb.hip_lib().orb_variant_odp
+            fn.restype = ctypes.c_int
+            nprobe = fn(buf.ctypes.data_as(ctypes.c_void_p), 512)
+            for i in range(min(nprobe, 16)):
+                o = buf[8 * i: 8 * i + 8]
+                got = o[3:7].view(np.float32)
+                print(f"  probe: wave {o[0] >> 16} lane {(o[0] >> 8) & 255} q {o[0] & 255} slot {o[1]} frame {o[2]} "
+                      f"block {o[7]} got {got.tolist()} bits {[hex(x) for x in o[3:7]]}")
+            if nprobe:
+                print(f"  probe records: {nprobe}")
         ko, do = ora.extract(img)
         if kg.tobytes() != ko.tobytes():
             print(f"frame {fi} rep {rep}: keypoints differ")

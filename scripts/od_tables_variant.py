@@ -45,6 +45,39 @@ elif mode == "drainexit":  # E1: waves without a keypoint drain their loads befo
     reps.append(("    if (!active) return;", "    if (!active) {\n        asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n        return;\n    }"))
 elif mode == "prewait":  # E2: compiler-placed pattern loads, every wave waits for them before the barrier
     reps.append(("    lds_barrier();  // s_trig is written", "    asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n    lds_barrier();  // s_trig is written"))
+elif mode == "probe":  # record every pattern register that differs from the table, after the second barrier
+    reps.append(("struct ODTables {", "__device__ uint32_t g_odp[8 * 512];\n__device__ uint32_t g_odpn;\nstruct ODTables {"))
+    reps.append(("    lds_barrier();  // s_trig is written (and the row-pass sums: LDS)\n    if (!active) return;",
+        "    lds_barrier();  // s_trig is written (and the row-pass sums: LDS)\n"
+        "    if (active) {\n"
+        "        asm volatile(\"s_waitcnt vmcnt(0)\" ::: \"memory\");\n"
+        "#pragma unroll\n"
+        "        for (int q = 0; q < 4; ++q) {\n"
+        "            float4 gg;\n"
+        "            asm volatile(\"global_load_dwordx4 %0, %1, %2 sc0 sc1\\n\\ts_waitcnt vmcnt(0)\" : \"=v\"(gg) : \"v\"(16u * (4u * (uint32_t)lane + q)), \"s\"(tb.patf) : \"memory\");\n"
+        "            if (gg.x != pat[4 * q] || gg.y != pat[4 * q + 1] || gg.z != pat[4 * q + 2] || gg.w != pat[4 * q + 3]) {\n"
+        "                const uint32_t i = atomicAdd(&g_odpn, 1u);\n"
+        "                if (i < 512) {\n"
+        "                    uint32_t* o = g_odp + 8 * i;\n"
+        "                    o[0] = ((uint32_t)wave << 16) | ((uint32_t)lane << 8) | (uint32_t)q; o[1] = (uint32_t)k; o[2] = (uint32_t)b;\n"
+        "                    o[3] = __float_as_uint(pat[4 * q]); o[4] = __float_as_uint(pat[4 * q + 1]);\n"
+        "                    o[5] = __float_as_uint(pat[4 * q + 2]); o[6] = __float_as_uint(pat[4 * q + 3]); o[7] = blockIdx.x;\n"
+        "                }\n"
+        "            }\n"
+        "        }\n"
+        "    }\n"
+        "    if (!active) return;"))
+    reps.append(("int orb_debug_kf_timing(unsigned long long* out6) {",
+        "extern \"C\" int orb_variant_odp(uint32_t* out, int n) {\n"
+        "    uint32_t cnt = 0;\n"
+        "    HIP_TRY(hipDeviceSynchronize());\n"
+        "    HIP_TRY(hipMemcpyFromSymbol(&cnt, HIP_SYMBOL(g_odpn), 4));\n"
+        "    if (out && n > 0) HIP_TRY(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_odp), 4u * 8u * (uint32_t)std::min(n, 512)));\n"
+        "    const uint32_t z = 0;\n"
+        "    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_odpn), &z, 4));\n"
+        "    return (int)cnt;\n"
+        "}\n"
+        "int orb_debug_kf_timing(unsigned long long* out6) {"))
 assert LOADLINE in reps[4][1] or mode in ("sc", "asmwait", "dw")
 args = ["python3", "scripts/ablation_variant.py", sys.argv[1]]
 for a, b in reps:
