@@ -361,7 +361,17 @@ def latency_b1(orb, W, H, NF, device, frames, reps=100):
         search_for_initialization(F1.mvKeys, F1.mDescriptors, F2.mvKeys, F2.mDescriptors, W, H, prev0.copy(), 0.9,
                                   True, 100)
     c_sfi = (time.perf_counter() - t0) / n_cpu
+    # the same entry points timed in C++ (build/latency_gpu, a child process: no Python in the
+    # loop), plus SearchByBoW(KF, F) and SearchByProjection(local map) per call
+    c_abi = None
+    exe = os.path.join(ROOT, "build", "latency_gpu")
+    if os.path.exists(exe):
+        r = subprocess.run([exe, str(W), str(H), str(NF), "200"], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                           text=True, timeout=120)
+        if r.returncode == 0:
+            c_abi = json.loads(r.stdout.strip().splitlines()[-1])
     return {
+        "c_abi_us": c_abi,
         "orb_extract_host_ms": t_ext * 1e3,
         "orb_extract_device_b1_ms": t_dev * 1e3,
         "search_for_initialization_host_ms": t_sfi * 1e3,

@@ -12,9 +12,10 @@
 // queries: nodes are independent and run in parallel (one wave per node), the queries of a node
 // in the reference's order.  Only the rotation filter is per pair.
 //
-// One 256-thread workgroup per pair:
+// One 1024-thread workgroup per pair (16 waves: 4 waves per pair left 2 waves per SIMD at 511
+// pairs, 0.388 ms per c3 step):
 //   1. each thread binary-searches KF node positions in the other vector's node list (LDS);
-//   2. wave w takes the common nodes w, w+4, ...: per query (wave-uniform) every lane scores the
+//   2. wave w takes the common nodes w, w+16, ...: per query (wave-uniform) every lane scores the
 //      node's candidates it holds (<= 64 candidates: one per lane, descriptor in registers for
 //      the whole node; more: strided, reloaded), key = (distance << 16) | candidate position, and
 //      two wave-min reductions give the reference's bestDist1 / bestIdx (first minimum in
@@ -37,6 +38,8 @@ namespace {
 
 constexpr int TH_LOW = 50, HISTO = 30;  // ORBmatcher.cc:40-42
 constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr int BOW_WAVES = 16;  // waves per pair: the common nodes are dealt round-robin to them
+constexpr int BOW_T = 64 * BOW_WAVES;
 
 __device__ __forceinline__ uint32_t wmin(uint32_t v) {
 #pragma unroll
@@ -74,7 +77,7 @@ struct BowBatch {
     float nnratio;
 };
 
-__global__ void __launch_bounds__(256) k_bow_pairs(BowBatch J) {
+__global__ void __launch_bounds__(BOW_T) k_bow_pairs(BowBatch J) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ int s_hist[HISTO];
     __shared__ int s_ind[3];
@@ -101,9 +104,9 @@ __global__ void __launch_bounds__(256) k_bow_pairs(BowBatch J) {
     int* s_mb = (int*)smem;                   // [cap] KF node position -> other node position or -1
     uint8_t* s_taken = smem + 4 * (size_t)cap;  // [cap] other-side features matched (or unusable)
 
-    for (int i = tid; i < cap; i += 256) out[i] = -1;
-    for (int i = tid; i < nB; i += 256) s_taken[i] = (J.kfkf && UB) ? (uint8_t)(UB[i] == 0) : (uint8_t)0;
-    for (int a = tid; a < nodesA; a += 256) {  // the merge walk's common nodes (lower_bound)
+    for (int i = tid; i < cap; i += BOW_T) out[i] = -1;
+    for (int i = tid; i < nB; i += BOW_T) s_taken[i] = (J.kfkf && UB) ? (uint8_t)(UB[i] == 0) : (uint8_t)0;
+    for (int a = tid; a < nodesA; a += BOW_T) {  // the merge walk's common nodes (lower_bound)
         const uint32_t id = NA[a];
         int lo = 0, hi = nodesB;
         while (lo < hi) {
@@ -120,7 +123,7 @@ __global__ void __launch_bounds__(256) k_bow_pairs(BowBatch J) {
     __syncthreads();
 
     int acc = 0;  // accepted by this wave (lane 0 counts)
-    for (int a = wave; a < nodesA; a += 4) {
+    for (int a = wave; a < nodesA; a += BOW_WAVES) {
         const int b = s_mb[a];
         if (b < 0) continue;
         const int q0 = OA[a], q1 = OA[a + 1], c0 = OB[b], nc = OB[b + 1] - c0;
@@ -134,11 +137,30 @@ __global__ void __launch_bounds__(256) k_bow_pairs(BowBatch J) {
             m0 = DB[2 * (size_t)myIdx];
             m1 = DB[2 * (size_t)myIdx + 1];
         }
+        // the node's queries 64 at a time: lane j loads query j's index, flag and descriptor (one
+        // global round trip per 64 queries), each query then takes them by v_readlane
+        int qIdx = 0, qOk = 0;
+        uint4 qd0 = make_uint4(0, 0, 0, 0), qd1 = qd0;
         for (int q = q0; q < q1; ++q) {
-            const int idx1 = __builtin_amdgcn_readfirstlane(FA[q]);
-            if ((unsigned)idx1 >= (unsigned)nA) continue;  // (not a feature of the frame: never from transform)
-            if (UA && !UA[idx1]) continue;  // !pMP || pMP->isBad()
-            const uint4 d0 = DA[2 * (size_t)idx1], d1 = DA[2 * (size_t)idx1 + 1];
+            const int j = (q - q0) & 63;
+            if (j == 0) {
+                qOk = 0;
+                if (q + lane < q1) {
+                    qIdx = FA[q + lane];
+                    // (an index outside the frame is never produced by transform; skipped)
+                    qOk = (unsigned)qIdx < (unsigned)nA && (!UA || UA[qIdx]);  // !pMP || pMP->isBad()
+                    const int qi = qOk ? qIdx : 0;
+                    qd0 = DA[2 * (size_t)qi];
+                    qd1 = DA[2 * (size_t)qi + 1];
+                }
+            }
+            if (!__builtin_amdgcn_readlane(qOk, j)) continue;
+            const int idx1 = __builtin_amdgcn_readlane(qIdx, j);
+            uint4 d0, d1;
+            d0.x = __builtin_amdgcn_readlane(qd0.x, j), d0.y = __builtin_amdgcn_readlane(qd0.y, j);
+            d0.z = __builtin_amdgcn_readlane(qd0.z, j), d0.w = __builtin_amdgcn_readlane(qd0.w, j);
+            d1.x = __builtin_amdgcn_readlane(qd1.x, j), d1.y = __builtin_amdgcn_readlane(qd1.y, j);
+            d1.z = __builtin_amdgcn_readlane(qd1.z, j), d1.w = __builtin_amdgcn_readlane(qd1.w, j);
             uint32_t k1 = NONE, k2 = NONE;  // this lane's two smallest keys
             if (small) {
                 if (lane < nc && !s_taken[myIdx]) k1 = ((uint32_t)ham(d0, d1, m0, m1) << 16) | (uint32_t)lane;
@@ -164,7 +186,7 @@ __global__ void __launch_bounds__(256) k_bow_pairs(BowBatch J) {
             const bool thOk = J.kfkf ? dist1 < TH_LOW : dist1 <= TH_LOW;
             if (!(thOk && (float)dist1 < J.nnratio * (float)dist2)) continue;
             const int jb = (int)(b1 & 0xFFFFu);
-            const int idx2 = small ? __shfl(myIdx, jb, 64) : FB[c0 + jb];
+            const int idx2 = small ? __builtin_amdgcn_readlane(myIdx, jb) : FB[c0 + jb];
             if (lane == 0) {
                 s_taken[idx2] = 1;
                 if (J.kfkf)
@@ -204,7 +226,7 @@ __global__ void __launch_bounds__(256) k_bow_pairs(BowBatch J) {
         }
         __syncthreads();
         int rem = 0;
-        for (int i = tid; i < nOut; i += 256) {
+        for (int i = tid; i < nOut; i += BOW_T) {
             const int v = out[i];
             if (v < 0) continue;
             const int bin = J.kfkf ? rot_bin(KA[i].angle, KB[v].angle) : rot_bin(KA[v].angle, KB[i].angle);
@@ -237,7 +259,7 @@ extern "C" int orb_search_by_bow_batch_device(int kf_kf, const orb_keypoint_t* d
     BowBatch J{d_kps, d_desc, d_counts, d_fv_nodes, d_fv_offsets, d_fv_features, d_fv_n, d_pair_a, d_pair_b,
                d_usable, d_match, d_nmatches, cap, kf_kf, check_ori ? 1 : 0, nnratio};
     const size_t lds = 5 * (size_t)cap;
-    hipLaunchKernelGGL(k_bow_pairs, dim3(P), dim3(256), lds, (hipStream_t)stream, J);
+    hipLaunchKernelGGL(k_bow_pairs, dim3(P), dim3(BOW_T), lds, (hipStream_t)stream, J);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return orb_internal_set_error(ORB_EDEVICE, std::string("k_bow_pairs: ") + hipGetErrorString(e));
     return ORB_OK;

@@ -4265,9 +4265,8 @@ int orb_search_for_initialization(const orb_keypoint_t* kps1, const uint8_t* des
     int st = orb_search_for_initialization_batch_device((const orb_keypoint_t*)(ds + oK), ds + oD, dc, cap, 1, dc + 2,
                                                         dc + 3, bounds, nnratio, check_ori, window, (float*)(ds + oP),
                                                         dm, dm + cap, s);
-    hipError_t e = hipSuccess;
-    if (!st) e = hipMemcpyAsync(hs + oP, ds + oP, (size_t)n1 * 8, hipMemcpyDeviceToHost, s);
-    if (!st && e == hipSuccess) e = hipMemcpyAsync(hs + oM, ds + oM, (size_t)cap * 4 + 4, hipMemcpyDeviceToHost, s);
+    hipError_t e = hipSuccess;  // vbPrevMatched and vnMatches12 + nmatches are adjacent: one D2H copy
+    if (!st) e = hipMemcpyAsync(hs + oP, ds + oP, oM + (size_t)cap * 4 + 4 - oP, hipMemcpyDeviceToHost, s);
     hipError_t es = hipStreamSynchronize(s);  // always drained: the staging is reused by the next call
     if (st) return st;
     if (e == hipSuccess) e = es;

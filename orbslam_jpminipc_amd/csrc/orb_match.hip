@@ -138,6 +138,7 @@ struct Job {
     const uint8_t* taken0;  // T.n exclusion flags on entry (NULL = none)
     QP* qp;
     uint32_t* topk;  // qn x TOPK
+    uint32_t* topx;  // qn x TOPK: target index | octave << 24 of each top-8 entry (k_query_scan)
     int* cnt;        // qn
     int* out;        // outN
     int outN, outByTarget;
@@ -539,7 +540,17 @@ __global__ void __launch_bounds__(256) k_query_scan(Job J) {
         }
         if (lane == k) res = mn;
     }
-    if (lane < TOPK) J.topk[(size_t)q * TOPK + lane] = res;
+    if (lane < TOPK) {
+        J.topk[(size_t)q * TOPK + lane] = res;
+        // the entry's target and its octave, so the loop-carried resolver reads no dependent
+        // global data per query
+        uint32_t x = 0;
+        if (res != 0xFFFFFFFFu) {
+            const int idx = key_idx(J, res);
+            x = (uint32_t)idx | ((uint32_t)J.T.kps[idx].octave << 24);
+        }
+        J.topx[(size_t)q * TOPK + lane] = x;
+    }
     if (lane == 0) J.cnt[q] = n;
 }
 
@@ -662,13 +673,17 @@ __device__ uint32_t triang_rescan(const Job& J, int q, const QP& p, const uint8_
     return wave_min(best);
 }
 
+// One instantiation per matcher (MODE == J.mode): the loop-carried pass of each is its own
+// straight-line code, without the other modes' branches.
+template <int MODE>
 __global__ void __launch_bounds__(256) k_resolve(Job J) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ int s_hist[HISTO + 2];
     __shared__ int s_ind[3];
     __shared__ int s_nacc;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int Tn = J.T.n, m = J.mode;
+    const int Tn = J.T.n;
+    constexpr int m = MODE;
     int* s_out = (int*)smem;                                  // outN
     int* s_acc = s_out + J.outN;                               // accepted: (slot << 5) | bin
     uint8_t* s_taken = (uint8_t*)(s_acc + max(Tn, 1));          // Tn
@@ -693,14 +708,27 @@ __global__ void __launch_bounds__(256) k_resolve(Job J) {
         atomicAdd(&s_nacc, acc);
     } else if (wave == 0) {
         int nacc = 0;
+        // A query's inputs (flags, candidate count, top-8 keys with their targets and octaves) do
+        // not depend on the loop-carried state, so query q + 1's are loaded while q is decided:
+        // the pass pays LDS round trips per query, not dependent global ones
+        int nFlags = 0, nCnt = 0;
+        uint32_t nE = 0xFFFFFFFFu, nX = 0;
+        auto fetch = [&](int q) {
+            nFlags = J.qp[q].flags;
+            nCnt = J.cnt[q];
+            nE = lane < TOPK ? J.topk[(size_t)q * TOPK + lane] : 0xFFFFFFFFu;
+            nX = lane < TOPK ? J.topx[(size_t)q * TOPK + lane] : 0u;
+        };
+        if (J.qn > 0) fetch(0);
         for (int q = 0; q < J.qn; ++q) {
-            const QP p = J.qp[q];
-            if (!(p.flags & 1)) continue;
-            const int cnt = J.cnt[q];
+            const int flags = nFlags, cnt = nCnt;
+            const uint32_t eL = nE, xL = nX;
+            if (q + 1 < J.qn) fetch(q + 1);
+            if (!(flags & 1)) continue;
             if (cnt == 0) continue;
             const int k = min(cnt, TOPK);
-            const uint32_t e = lane < k ? J.topk[(size_t)q * TOPK + lane] : 0xFFFFFFFFu;
-            const int eidx = lane < k ? key_idx(J, e) : 0;
+            const uint32_t e = lane < k ? eL : 0xFFFFFFFFu;
+            const int eidx = lane < k ? (int)(xL & 0xFFFFFFu) : 0;
             const bool untaken = lane < k && !s_taken[eidx];
             const uint64_t um = __ballot(untaken);
             int bestIdx = -1, bestDist = INT_MAX, bestDist2 = INT_MAX, bestLevel = -1, bestLevel2 = -1;
@@ -713,7 +741,7 @@ __global__ void __launch_bounds__(256) k_resolve(Job J) {
                     const int first = __ffsll((unsigned long long)um) - 1;
                     const int distTh = 2 * (int)(__shfl(e, first, 64) >> 16);
                     const orb_keypoint_t kp1 = J.qkps[qrow(J, q)];
-                    const bool inTh = lane < k && (int)(e >> 16) <= distTh;
+                    const bool inTh = lane < k && (int)(e >> 16) <= distTh;  // (epipolar: the target's point, below)
                     const bool pass = untaken && inTh && epipolar_ok(J, kp1, J.T.kps[eidx]);
                     const uint64_t pm = __ballot(pass), om = __ballot(lane < k && !inTh);
                     if (pm != 0ull) {
@@ -725,29 +753,45 @@ __global__ void __launch_bounds__(256) k_resolve(Job J) {
                 } else if (cnt <= TOPK) {
                     decided = true;
                 }
-                if (!decided) chosen = triang_rescan(J, q, p, s_taken, lane);
+                if (!decided) chosen = triang_rescan(J, q, J.qp[q], s_taken, lane);
                 if (chosen == 0xFFFFFFFFu) continue;
                 bestIdx = key_idx(J, chosen);
                 bestDist = 0;  // accepted below unconditionally
             } else {
                 const int need = needs_second(m) ? 2 : 1;
                 uint32_t b1 = 0xFFFFFFFFu, b2 = 0xFFFFFFFFu;
+                uint32_t x1 = 0u, x2 = 0u;
                 if (__popcll(um) >= need || cnt <= TOPK) {
                     if (um != 0ull) {
-                        b1 = __shfl(e, __ffsll((unsigned long long)um) - 1, 64);
+                        // (wave-uniform lanes: v_readlane, no LDS round trip)
+                        const int l1 = __ffsll((unsigned long long)um) - 1;
+                        b1 = (uint32_t)__builtin_amdgcn_readlane((int)e, l1);
+                        x1 = (uint32_t)__builtin_amdgcn_readlane((int)xL, l1);
                         const uint64_t um2 = um & (um - 1);
-                        if (um2) b2 = __shfl(e, __ffsll((unsigned long long)um2) - 1, 64);
+                        if (um2) {
+                            const int l2 = __ffsll((unsigned long long)um2) - 1;
+                            b2 = (uint32_t)__builtin_amdgcn_readlane((int)e, l2);
+                            x2 = (uint32_t)__builtin_amdgcn_readlane((int)xL, l2);
+                        }
                     }
                 } else {
-                    rescan_best2(J, q, p, s_taken, lane, &b1, &b2);
+                    rescan_best2(J, q, J.qp[q], s_taken, lane, &b1, &b2);
+                    if (b1 != 0xFFFFFFFFu) {
+                        const int i1x = key_idx(J, b1);
+                        x1 = (uint32_t)i1x | ((uint32_t)J.T.kps[i1x].octave << 24);
+                    }
+                    if (b2 != 0xFFFFFFFFu) {
+                        const int i2x = key_idx(J, b2);
+                        x2 = (uint32_t)i2x | ((uint32_t)J.T.kps[i2x].octave << 24);
+                    }
                 }
                 if (b1 == 0xFFFFFFFFu) continue;  // every candidate taken: bestDist stays INT_MAX
-                bestIdx = key_idx(J, b1);
+                bestIdx = (int)(x1 & 0xFFFFFFu);
                 bestDist = (int)(b1 >> 16);
-                bestLevel = J.T.kps[bestIdx].octave;
+                bestLevel = (int)(x1 >> 24);
                 if (b2 != 0xFFFFFFFFu) {
                     bestDist2 = (int)(b2 >> 16);
-                    bestLevel2 = J.T.kps[key_idx(J, b2)].octave;
+                    bestLevel2 = (int)(x2 >> 24);
                 }
             }
             bool accept = false;
@@ -785,10 +829,7 @@ __global__ void __launch_bounds__(256) k_resolve(Job J) {
                 const int qv = qrow(J, q);
                 const int slot = J.outByTarget ? bestIdx : qv;
                 s_out[slot] = J.outByTarget ? qv : bestIdx;
-                if (rotMode) {
-                    const float a1 = J.qkps[qv].angle, a2 = J.T.kps[bestIdx].angle;
-                    s_acc[nacc] = (slot << 5) | rot_bin(a1, a2);
-                }
+                if (rotMode) s_acc[nacc] = slot << 5;  // its rotation bin: after the pass, in parallel
             }
             ++nacc;
             // lane 0's LDS writes land before any lane's next read (same wave, in order)
@@ -802,7 +843,13 @@ __global__ void __launch_bounds__(256) k_resolve(Job J) {
         const int nacc = s_nacc;
         if (tid < HISTO) s_hist[tid] = 0;
         __syncthreads();
-        for (int i = tid; i < nacc; i += 256) atomicAdd(&s_hist[s_acc[i] & 31], 1);
+        for (int i = tid; i < nacc; i += 256) {
+            const int slot = s_acc[i] >> 5, v = s_out[slot];
+            const int qv = J.outByTarget ? v : slot, ti = J.outByTarget ? slot : v;
+            const int bin = rot_bin(J.qkps[qv].angle, J.T.kps[ti].angle);
+            s_acc[i] = (slot << 5) | bin;
+            atomicAdd(&s_hist[bin], 1);
+        }
         __syncthreads();
         if (tid == 0) {  // ComputeThreeMaxima (1748-1789)
             int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
@@ -959,6 +1006,9 @@ struct Arena {
         if (host && bytes) uploads.push_back({off, {host, bytes}});
         return off;
     }
+    void put(size_t off, const void* host, size_t bytes) {  // into a region from take()
+        if (host && bytes) uploads.push_back({off, {host, bytes}});
+    }
 };
 
 struct DeviceGuard {
@@ -1101,12 +1151,13 @@ int launch_grid(const Call& C, const DView& d) {
 
 // Scratch of a job: qp, topk, cnt (+ outputs).
 struct JobOffs {
-    size_t qp, topk, cnt, out, nOut;
+    size_t qp, topk, topx, cnt, out, nOut;
 };
 JobOffs plan_job(Arena& A, int qn, int outN) {
     JobOffs o{};
     o.qp = A.take((size_t)std::max(qn, 1) * sizeof(QP));
     o.topk = A.take((size_t)std::max(qn, 1) * TOPK * 4);
+    o.topx = A.take((size_t)std::max(qn, 1) * TOPK * 4);
     o.cnt = A.take((size_t)std::max(qn, 1) * 4);
     o.out = A.take((size_t)std::max(outN, 1) * 4);
     o.nOut = A.take(16);
@@ -1116,6 +1167,7 @@ void bind_job(const Call& C, Job& J, const JobOffs& o, int qn, int outN) {
     J.qn = qn;
     J.qp = C.at<QP>(o.qp);
     J.topk = C.at<uint32_t>(o.topk);
+    J.topx = C.at<uint32_t>(o.topx);
     J.cnt = C.at<int>(o.cnt);
     J.out = C.at<int>(o.out);
     J.outN = outN;
@@ -1139,10 +1191,41 @@ int run_job(const Call& C, const Job& J) {
     if (st) return st;
     static std::atomic<bool> attr_set[64] = {};
     if (!attr_set[C.device].load()) {
-        HIPCHK(hipFuncSetAttribute((const void*)k_resolve, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
+#define SET_RESOLVE_LDS(M) HIPCHK(hipFuncSetAttribute((const void*)k_resolve<M>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024))
+        SET_RESOLVE_LDS(M_LOCAL);
+        SET_RESOLVE_LDS(M_WINDOW);
+        SET_RESOLVE_LDS(M_F2F);
+        SET_RESOLVE_LDS(M_MOTION);
+        SET_RESOLVE_LDS(M_RELOC);
+        SET_RESOLVE_LDS(M_SIM3P);
+        SET_RESOLVE_LDS(M_FUSE);
+        SET_RESOLVE_LDS(M_FUSE_SCW);
+        SET_RESOLVE_LDS(M_SIM3);
+        SET_RESOLVE_LDS(M_BOW_KFF);
+        SET_RESOLVE_LDS(M_BOW_KFKF);
+        SET_RESOLVE_LDS(M_TRIANG);
+#undef SET_RESOLVE_LDS
         attr_set[C.device] = true;
     }
-    hipLaunchKernelGGL(k_resolve, dim3(1), dim3(256), lds, s, J);
+    switch (J.mode) {
+#define LAUNCH_RESOLVE(M) \
+    case M: hipLaunchKernelGGL(k_resolve<M>, dim3(1), dim3(256), lds, s, J); break;
+        LAUNCH_RESOLVE(M_LOCAL)
+        LAUNCH_RESOLVE(M_WINDOW)
+        LAUNCH_RESOLVE(M_F2F)
+        LAUNCH_RESOLVE(M_MOTION)
+        LAUNCH_RESOLVE(M_RELOC)
+        LAUNCH_RESOLVE(M_SIM3P)
+        LAUNCH_RESOLVE(M_FUSE)
+        LAUNCH_RESOLVE(M_FUSE_SCW)
+        LAUNCH_RESOLVE(M_SIM3)
+        LAUNCH_RESOLVE(M_BOW_KFF)
+        LAUNCH_RESOLVE(M_BOW_KFKF)
+        LAUNCH_RESOLVE(M_TRIANG)
+#undef LAUNCH_RESOLVE
+        default:
+            return fail(ORB_EINVAL, "matcher mode without a resolver");
+    }
     HIPCHK(hipGetLastError());
     return ORB_OK;
 }
@@ -1170,6 +1253,69 @@ bool bad_fv(const orb_feature_vector_t& f, int n) {
     return f.offsets[f.n_nodes] > 65535;
 }
 
+// Every feature index at most once in the FeatureVector and no node without features (what
+// TemplatedVocabulary::transform builds: FeatureVector::addFeature once per feature).
+bool unique_fv(const orb_feature_vector_t& f, int n) {
+    std::vector<uint8_t> seen((size_t)std::max(n, 1), 0);
+    for (int a = 0; a < f.n_nodes; ++a) {
+        if (f.offsets[a + 1] == f.offsets[a]) return false;
+        for (int i = f.offsets[a]; i < f.offsets[a + 1]; ++i) {
+            if (seen[f.features[i]]) return false;
+            seen[f.features[i]] = 1;
+        }
+    }
+    return true;
+}
+
+// SearchByBoW (KF-F / KF-KF) of one pair through the batched node-parallel kernel
+// (csrc/orb_bow.hip, P = 1): the two frames staged in its [2][cap] layout, one H2D copy, one
+// launch, one D2H copy.  (The generic path below replays every query on one wave.)
+int bow_match_nodes(int mode, const orb_frame_view_t* V1, const uint8_t* flag1, const orb_feature_vector_t& fv1,
+                    const orb_frame_view_t* V2, const uint8_t* flag2, const orb_feature_vector_t& fv2, float nnratio,
+                    int check_ori, int32_t* out, int outN, int* n_out, int device) {
+    int st;
+    Call C{device};
+    if ((st = C.begin())) return st;
+    DeviceGuard dg(device);
+    Arena& A = C.A;
+    const int cap = std::max(V1->n, V2->n);
+    const int counts[2] = {V1->n, V2->n}, fvn[2] = {fv1.n_nodes, fv2.n_nodes}, pair[2] = {0, 1};
+    const size_t oK = A.take((size_t)2 * cap * sizeof(orb_keypoint_t));
+    A.put(oK, V1->kps, (size_t)V1->n * sizeof(orb_keypoint_t));
+    A.put(oK + (size_t)cap * sizeof(orb_keypoint_t), V2->kps, (size_t)V2->n * sizeof(orb_keypoint_t));
+    const size_t oD = A.take((size_t)2 * cap * 32);
+    A.put(oD, V1->desc, (size_t)V1->n * 32);
+    A.put(oD + (size_t)cap * 32, V2->desc, (size_t)V2->n * 32);
+    const size_t oC = A.stage(counts, sizeof(counts));
+    const size_t oN = A.take((size_t)2 * cap * 4);
+    A.put(oN, fv1.nodes, (size_t)fv1.n_nodes * 4);
+    A.put(oN + (size_t)cap * 4, fv2.nodes, (size_t)fv2.n_nodes * 4);
+    const size_t oO = A.take((size_t)2 * (cap + 1) * 4);
+    A.put(oO, fv1.offsets, (size_t)(fv1.n_nodes + 1) * 4);
+    A.put(oO + (size_t)(cap + 1) * 4, fv2.offsets, (size_t)(fv2.n_nodes + 1) * 4);
+    const size_t oF = A.take((size_t)2 * cap * 4);
+    A.put(oF, fv1.features, (size_t)fv1.offsets[fv1.n_nodes] * 4);
+    A.put(oF + (size_t)cap * 4, fv2.features, (size_t)fv2.offsets[fv2.n_nodes] * 4);
+    const size_t oV = A.stage(fvn, sizeof(fvn));
+    const size_t oP = A.stage(pair, sizeof(pair));
+    const size_t oU = A.take((size_t)2 * cap);
+    A.put(oU, flag1, (size_t)V1->n);
+    if (flag2) A.put(oU + (size_t)cap, flag2, (size_t)V2->n);
+    const size_t oM = A.take((size_t)cap * 4 + 4);
+    if ((st = C.commit())) return st;
+    st = orb_search_by_bow_batch_device(mode == M_BOW_KFKF, C.at<orb_keypoint_t>(oK), C.at<uint8_t>(oD), C.at<int32_t>(oC),
+                                        cap, C.at<uint32_t>(oN), C.at<int32_t>(oO), C.at<int32_t>(oF), C.at<int32_t>(oV), 1,
+                                        C.at<int32_t>(oP), C.at<int32_t>(oP) + 1, C.at<uint8_t>(oU), nnratio, check_ori,
+                                        C.at<int32_t>(oM), C.at<int32_t>(oM) + cap, C.ctx->stream);
+    if (st) return st;
+    int nm = 0;
+    if ((st = C.download(out, oM, (size_t)outN * 4)) || (st = C.download(&nm, oM + (size_t)cap * 4, 4)) ||
+        (st = C.sync()))
+        return st;
+    *n_out = nm;
+    return ORB_OK;
+}
+
 // Shared driver of the three BoW matchers.
 int bow_match(int mode, const orb_frame_view_t* V1, const uint8_t* flag1, orb_feature_vector_t fv1,
               const orb_frame_view_t* V2, const uint8_t* flag2, orb_feature_vector_t fv2, const float* F12,
@@ -1186,6 +1332,9 @@ int bow_match(int mode, const orb_frame_view_t* V1, const uint8_t* flag1, orb_fe
         for (int i = 0; i < outN; ++i) out[i] = -1;
         return ORB_OK;
     }
+    if (mode != M_TRIANG && std::max(V1->n, V2->n) <= 8192 && fv1.n_nodes <= V1->n && fv2.n_nodes <= V2->n &&
+        unique_fv(fv1, V1->n) && unique_fv(fv2, V2->n))
+        return bow_match_nodes(mode, V1, flag1, fv1, V2, flag2, fv2, nnratio, check_ori, out, outN, n_out, device);
     const int qn = fv1.offsets[fv1.n_nodes];
     Call C{device};
     if ((st = C.begin())) return st;

@@ -3,7 +3,9 @@
 test_extract_parity_configs[W-H-nf] with the library named by ORB_HIP_LIB (or the in-tree one)
 and the oracle, and print, per differing descriptor row, the keypoint, its window alignment and
 the differing rBRIEF tests (test i = pattern points 2i, 2i+1; lane i // 4 of k_orient_desc).
-Usage: od_diag.py [W H nf [reps]]"""
+Usage: od_diag.py [W H nf [reps]]; ORB_DIAG_SELF=1 compares every repetition with the first
+GPU run of the frame instead of the oracle (run-to-run nondeterminism of wrong-output builds)."""
+import os
 import pathlib
 import sys
 
@@ -38,6 +40,12 @@ for fi, img in enumerate(orb.synth_stream(W, H, stream=3, first=0, count=3)):
             if nprobe:
                 print(f"  probe records: {nprobe}")
         ko, do = ora.extract(img)
+        if os.environ.get("ORB_DIAG_SELF"):
+            if rep == 0:
+                ko, do = kg.copy(), (dg.copy() if dg is not None else None)
+                first = (ko, do)
+            else:
+                ko, do = first
         if kg.tobytes() != ko.tobytes():
             print(f"frame {fi} rep {rep}: keypoints differ")
             continue

@@ -78,6 +78,18 @@ elif mode == "probe":  # record every pattern register that differs from the tab
         "    return (int)cnt;\n"
         "}\n"
         "int orb_debug_kf_timing(unsigned long long* out6) {"))
+elif mode == "trig3":  # the workgroup's angle arithmetic on wave 3 instead of wave 0
+    reps.append(("    if (wave == 0 && lane < OD_WAVES) {", "    if (wave == 3 && lane < OD_WAVES) {"))
+elif mode == "nof64":  # (wrong output) the angle's sin / cos by a float polynomial: no f64 in the trig wave
+    reps.append(("        glibc_sincosf(ang * factorPI, &sa, &ca);",
+                 "        { const float xx = ang * factorPI - 3.14159265f, x2 = xx * xx; sa = -xx * (1.f - x2 * (1.f / 6.f - x2 * (1.f / 120.f))); ca = -(1.f - x2 * (0.5f - x2 * (1.f / 24.f))); }"))
+elif mode == "nodiv":  # (wrong output) fastAtan2 without its division (no v_div_scale / v_rcp in the trig wave)
+    reps.append(("        const float ang = fast_atan2((float)mm.x, (float)mm.y);",
+                 "        const float ang = fminf(fabsf((float)mm.x * 1e-3f + (float)mm.y * 2e-3f), 359.f);"))
+elif mode == "notrig":  # (wrong output) no angle arithmetic at all: a constant angle of each slot's moments
+    reps.append(("        const float ang = fast_atan2((float)mm.x, (float)mm.y);",
+                 "        const float ang = fminf(fabsf((float)mm.x * 1e-3f + (float)mm.y * 2e-3f), 359.f);"))
+    reps.append(("        glibc_sincosf(ang * factorPI, &sa, &ca);", "        sa = ang * 1e-3f; ca = 1.f - sa;"))
 assert LOADLINE in reps[4][1] or mode in ("sc", "asmwait", "dw")
 args = ["python3", "scripts/ablation_variant.py", sys.argv[1]]
 for a, b in reps:
