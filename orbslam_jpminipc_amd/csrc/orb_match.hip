@@ -608,6 +608,7 @@ __global__ void __launch_bounds__(256) k_area_fill(Job J) {
 }
 
 // ---- k_resolve -------------------------------------------------------------------------
+constexpr int RES_CHUNK = 64;  // queries staged per chunk of the sequential pass
 // Exact rescan of query q against the live taken flags: the two smallest keys.
 __device__ void rescan_best2(const Job& J, int q, const QP& p, const uint8_t* s_taken, int lane, uint32_t* b1,
                              uint32_t* b2) {
@@ -681,6 +682,9 @@ __global__ void __launch_bounds__(256) k_resolve(Job J) {
     __shared__ int s_hist[HISTO + 2];
     __shared__ int s_ind[3];
     __shared__ int s_nacc;
+    // the sequential pass's inputs, RES_CHUNK queries per buffer (double-buffered)
+    __shared__ int2 s_cq[2][RES_CHUNK];
+    __shared__ uint32_t s_ce[2][RES_CHUNK * TOPK], s_cx[2][RES_CHUNK * TOPK];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int Tn = J.T.n;
     constexpr int m = MODE;
@@ -706,136 +710,152 @@ __global__ void __launch_bounds__(256) k_resolve(Job J) {
             }
         }
         atomicAdd(&s_nacc, acc);
-    } else if (wave == 0) {
-        int nacc = 0;
+    } else {
         // A query's inputs (flags, candidate count, top-8 keys with their targets and octaves) do
-        // not depend on the loop-carried state, so query q + 1's are loaded while q is decided:
-        // the pass pays LDS round trips per query, not dependent global ones
-        int nFlags = 0, nCnt = 0;
-        uint32_t nE = 0xFFFFFFFFu, nX = 0;
-        auto fetch = [&](int q) {
-            nFlags = J.qp[q].flags;
-            nCnt = J.cnt[q];
-            nE = lane < TOPK ? J.topk[(size_t)q * TOPK + lane] : 0xFFFFFFFFu;
-            nX = lane < TOPK ? J.topx[(size_t)q * TOPK + lane] : 0u;
+        // not depend on the loop-carried state: waves 1-3 stage the next RES_CHUNK queries' inputs
+        // in LDS (double-buffered, one barrier per chunk) while wave 0 decides the current ones
+        // from LDS, so the sequential pass pays LDS round trips per query, no global ones
+        int nacc = 0;
+        const int nch = (J.qn + RES_CHUNK - 1) / RES_CHUNK;
+        auto load_chunk = [&](int c, int buf) {  // waves 1-3
+            for (int i = tid - 64; i < RES_CHUNK * TOPK; i += 192) {
+                const int q = c * RES_CHUNK + (i >> 3);
+                s_ce[buf][i] = q < J.qn ? J.topk[(size_t)q * TOPK + (i & 7)] : 0xFFFFFFFFu;
+                s_cx[buf][i] = q < J.qn ? J.topx[(size_t)q * TOPK + (i & 7)] : 0u;
+            }
+            for (int i = tid - 64; i < RES_CHUNK; i += 192) {
+                const int q = c * RES_CHUNK + i;
+                s_cq[buf][i] = q < J.qn ? make_int2(J.qp[q].flags, J.cnt[q]) : make_int2(0, 0);
+            }
         };
-        if (J.qn > 0) fetch(0);
-        for (int q = 0; q < J.qn; ++q) {
-            const int flags = nFlags, cnt = nCnt;
-            const uint32_t eL = nE, xL = nX;
-            if (q + 1 < J.qn) fetch(q + 1);
-            if (!(flags & 1)) continue;
-            if (cnt == 0) continue;
-            const int k = min(cnt, TOPK);
-            const uint32_t e = lane < k ? eL : 0xFFFFFFFFu;
-            const int eidx = lane < k ? (int)(xL & 0xFFFFFFu) : 0;
-            const bool untaken = lane < k && !s_taken[eidx];
-            const uint64_t um = __ballot(untaken);
-            int bestIdx = -1, bestDist = INT_MAX, bestDist2 = INT_MAX, bestLevel = -1, bestLevel2 = -1;
-            if (m == M_TRIANG) {
-                // walk the sorted list: BestDist from the first untaken entry, then the first
-                // untaken entry within round(2*BestDist) that passes the epipolar test
-                uint32_t chosen = 0xFFFFFFFFu;
-                bool decided = false;
-                if (um != 0ull) {
-                    const int first = __ffsll((unsigned long long)um) - 1;
-                    const int distTh = 2 * (int)(__shfl(e, first, 64) >> 16);
-                    const orb_keypoint_t kp1 = J.qkps[qrow(J, q)];
-                    const bool inTh = lane < k && (int)(e >> 16) <= distTh;  // (epipolar: the target's point, below)
-                    const bool pass = untaken && inTh && epipolar_ok(J, kp1, J.T.kps[eidx]);
-                    const uint64_t pm = __ballot(pass), om = __ballot(lane < k && !inTh);
-                    if (pm != 0ull) {
-                        chosen = __shfl(e, __ffsll((unsigned long long)pm) - 1, 64);
-                        decided = true;
-                    } else if (om != 0ull || cnt <= TOPK) {
-                        decided = true;  // the walk breaks on an entry past DistTh, or ends
-                    }
-                } else if (cnt <= TOPK) {
-                    decided = true;
-                }
-                if (!decided) chosen = triang_rescan(J, q, J.qp[q], s_taken, lane);
-                if (chosen == 0xFFFFFFFFu) continue;
-                bestIdx = key_idx(J, chosen);
-                bestDist = 0;  // accepted below unconditionally
+        if (wave != 0 && nch > 0) load_chunk(0, 0);
+        __syncthreads();
+        for (int c = 0; c < nch; ++c) {
+            if (wave != 0) {
+                if (c + 1 < nch) load_chunk(c + 1, (c + 1) & 1);
             } else {
-                const int need = needs_second(m) ? 2 : 1;
-                uint32_t b1 = 0xFFFFFFFFu, b2 = 0xFFFFFFFFu;
-                uint32_t x1 = 0u, x2 = 0u;
-                if (__popcll(um) >= need || cnt <= TOPK) {
-                    if (um != 0ull) {
-                        // (wave-uniform lanes: v_readlane, no LDS round trip)
-                        const int l1 = __ffsll((unsigned long long)um) - 1;
-                        b1 = (uint32_t)__builtin_amdgcn_readlane((int)e, l1);
-                        x1 = (uint32_t)__builtin_amdgcn_readlane((int)xL, l1);
-                        const uint64_t um2 = um & (um - 1);
-                        if (um2) {
-                            const int l2 = __ffsll((unsigned long long)um2) - 1;
-                            b2 = (uint32_t)__builtin_amdgcn_readlane((int)e, l2);
-                            x2 = (uint32_t)__builtin_amdgcn_readlane((int)xL, l2);
+                const int buf = c & 1, qend = min(RES_CHUNK, J.qn - c * RES_CHUNK);
+                for (int jq = 0; jq < qend; ++jq) {
+                    const int q = c * RES_CHUNK + jq;
+                    const int2 fc = s_cq[buf][jq];
+                    const int flags = __builtin_amdgcn_readfirstlane(fc.x), cnt = __builtin_amdgcn_readfirstlane(fc.y);
+                    if (!(flags & 1)) continue;
+                    if (cnt == 0) continue;
+                    const uint32_t eL = lane < TOPK ? s_ce[buf][jq * TOPK + lane] : 0xFFFFFFFFu;
+                    const uint32_t xL = lane < TOPK ? s_cx[buf][jq * TOPK + lane] : 0u;
+                    const int k = min(cnt, TOPK);
+                    const uint32_t e = lane < k ? eL : 0xFFFFFFFFu;
+                    const int eidx = lane < k ? (int)(xL & 0xFFFFFFu) : 0;
+                    const bool untaken = lane < k && !s_taken[eidx];
+                    const uint64_t um = __ballot(untaken);
+                    int bestIdx = -1, bestDist = INT_MAX, bestDist2 = INT_MAX, bestLevel = -1, bestLevel2 = -1;
+                    if (m == M_TRIANG) {
+                        // walk the sorted list: BestDist from the first untaken entry, then the first
+                        // untaken entry within round(2*BestDist) that passes the epipolar test
+                        uint32_t chosen = 0xFFFFFFFFu;
+                        bool decided = false;
+                        if (um != 0ull) {
+                            const int first = __ffsll((unsigned long long)um) - 1;
+                            const int distTh = 2 * (int)(__shfl(e, first, 64) >> 16);
+                            const orb_keypoint_t kp1 = J.qkps[qrow(J, q)];
+                            const bool inTh = lane < k && (int)(e >> 16) <= distTh;  // (epipolar: the target's point, below)
+                            const bool pass = untaken && inTh && epipolar_ok(J, kp1, J.T.kps[eidx]);
+                            const uint64_t pm = __ballot(pass), om = __ballot(lane < k && !inTh);
+                            if (pm != 0ull) {
+                                chosen = __shfl(e, __ffsll((unsigned long long)pm) - 1, 64);
+                                decided = true;
+                            } else if (om != 0ull || cnt <= TOPK) {
+                                decided = true;  // the walk breaks on an entry past DistTh, or ends
+                            }
+                        } else if (cnt <= TOPK) {
+                            decided = true;
+                        }
+                        if (!decided) chosen = triang_rescan(J, q, J.qp[q], s_taken, lane);
+                        if (chosen == 0xFFFFFFFFu) continue;
+                        bestIdx = key_idx(J, chosen);
+                        bestDist = 0;  // accepted below unconditionally
+                    } else {
+                        const int need = needs_second(m) ? 2 : 1;
+                        uint32_t b1 = 0xFFFFFFFFu, b2 = 0xFFFFFFFFu;
+                        uint32_t x1 = 0u, x2 = 0u;
+                        if (__popcll(um) >= need || cnt <= TOPK) {
+                            if (um != 0ull) {
+                                // (wave-uniform lanes: v_readlane, no LDS round trip)
+                                const int l1 = __ffsll((unsigned long long)um) - 1;
+                                b1 = (uint32_t)__builtin_amdgcn_readlane((int)e, l1);
+                                x1 = (uint32_t)__builtin_amdgcn_readlane((int)xL, l1);
+                                const uint64_t um2 = um & (um - 1);
+                                if (um2) {
+                                    const int l2 = __ffsll((unsigned long long)um2) - 1;
+                                    b2 = (uint32_t)__builtin_amdgcn_readlane((int)e, l2);
+                                    x2 = (uint32_t)__builtin_amdgcn_readlane((int)xL, l2);
+                                }
+                            }
+                        } else {
+                            rescan_best2(J, q, J.qp[q], s_taken, lane, &b1, &b2);
+                            if (b1 != 0xFFFFFFFFu) {
+                                const int i1x = key_idx(J, b1);
+                                x1 = (uint32_t)i1x | ((uint32_t)J.T.kps[i1x].octave << 24);
+                            }
+                            if (b2 != 0xFFFFFFFFu) {
+                                const int i2x = key_idx(J, b2);
+                                x2 = (uint32_t)i2x | ((uint32_t)J.T.kps[i2x].octave << 24);
+                            }
+                        }
+                        if (b1 == 0xFFFFFFFFu) continue;  // every candidate taken: bestDist stays INT_MAX
+                        bestIdx = (int)(x1 & 0xFFFFFFu);
+                        bestDist = (int)(b1 >> 16);
+                        bestLevel = (int)(x1 >> 24);
+                        if (b2 != 0xFFFFFFFFu) {
+                            bestDist2 = (int)(b2 >> 16);
+                            bestLevel2 = (int)(x2 >> 24);
                         }
                     }
-                } else {
-                    rescan_best2(J, q, J.qp[q], s_taken, lane, &b1, &b2);
-                    if (b1 != 0xFFFFFFFFu) {
-                        const int i1x = key_idx(J, b1);
-                        x1 = (uint32_t)i1x | ((uint32_t)J.T.kps[i1x].octave << 24);
+                    bool accept = false;
+                    switch (m) {
+                        case M_LOCAL:  // 112-121
+                            accept = bestDist <= TH_HIGH &&
+                                     !(bestLevel == bestLevel2 && (float)bestDist > J.nnratio * (float)bestDist2);
+                            break;
+                        case M_WINDOW:  // 476
+                        case M_F2F:     // 585
+                            accept = (float)bestDist <= (float)bestDist2 * J.nnratio && bestDist <= TH_HIGH;
+                            break;
+                        case M_BOW_KFF:  // 222-226
+                            accept = bestDist <= TH_LOW && (float)bestDist < J.nnratio * (float)bestDist2;
+                            break;
+                        case M_BOW_KFKF:  // 789-793
+                            accept = bestDist < TH_LOW && (float)bestDist < J.nnratio * (float)bestDist2;
+                            break;
+                        case M_MOTION:  // 1576
+                            accept = bestDist <= TH_HIGH;
+                            break;
+                        case M_RELOC:  // 1701
+                        case M_SIM3P:  // 393
+                            accept = bestDist <= J.thDist;
+                            break;
+                        case M_TRIANG:
+                            accept = true;
+                            break;
+                        default:
+                            break;
                     }
-                    if (b2 != 0xFFFFFFFFu) {
-                        const int i2x = key_idx(J, b2);
-                        x2 = (uint32_t)i2x | ((uint32_t)J.T.kps[i2x].octave << 24);
+                    if (!accept) continue;
+                    if (lane == 0) {
+                        s_taken[bestIdx] = 1;
+                        const int qv = qrow(J, q);
+                        const int slot = J.outByTarget ? bestIdx : qv;
+                        s_out[slot] = J.outByTarget ? qv : bestIdx;
+                        if (rotMode) s_acc[nacc] = slot << 5;  // its rotation bin: after the pass, in parallel
                     }
-                }
-                if (b1 == 0xFFFFFFFFu) continue;  // every candidate taken: bestDist stays INT_MAX
-                bestIdx = (int)(x1 & 0xFFFFFFu);
-                bestDist = (int)(b1 >> 16);
-                bestLevel = (int)(x1 >> 24);
-                if (b2 != 0xFFFFFFFFu) {
-                    bestDist2 = (int)(b2 >> 16);
-                    bestLevel2 = (int)(x2 >> 24);
+                    ++nacc;
+                    // lane 0's LDS writes land before any lane's next read (same wave, in order)
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
                 }
             }
-            bool accept = false;
-            switch (m) {
-                case M_LOCAL:  // 112-121
-                    accept = bestDist <= TH_HIGH &&
-                             !(bestLevel == bestLevel2 && (float)bestDist > J.nnratio * (float)bestDist2);
-                    break;
-                case M_WINDOW:  // 476
-                case M_F2F:     // 585
-                    accept = (float)bestDist <= (float)bestDist2 * J.nnratio && bestDist <= TH_HIGH;
-                    break;
-                case M_BOW_KFF:  // 222-226
-                    accept = bestDist <= TH_LOW && (float)bestDist < J.nnratio * (float)bestDist2;
-                    break;
-                case M_BOW_KFKF:  // 789-793
-                    accept = bestDist < TH_LOW && (float)bestDist < J.nnratio * (float)bestDist2;
-                    break;
-                case M_MOTION:  // 1576
-                    accept = bestDist <= TH_HIGH;
-                    break;
-                case M_RELOC:  // 1701
-                case M_SIM3P:  // 393
-                    accept = bestDist <= J.thDist;
-                    break;
-                case M_TRIANG:
-                    accept = true;
-                    break;
-                default:
-                    break;
-            }
-            if (!accept) continue;
-            if (lane == 0) {
-                s_taken[bestIdx] = 1;
-                const int qv = qrow(J, q);
-                const int slot = J.outByTarget ? bestIdx : qv;
-                s_out[slot] = J.outByTarget ? qv : bestIdx;
-                if (rotMode) s_acc[nacc] = slot << 5;  // its rotation bin: after the pass, in parallel
-            }
-            ++nacc;
-            // lane 0's LDS writes land before any lane's next read (same wave, in order)
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __syncthreads();  // chunk c decided, chunk c + 1 staged
         }
-        if (lane == 0) s_nacc = nacc;
+        if (wave == 0 && lane == 0) s_nacc = nacc;
     }
     __syncthreads();
     int removed = 0;

@@ -48,6 +48,10 @@ per = {n: out[i] / max(waves, 1) / max(nr.value, 1) for i, n in enumerate(names)
 print(f"{a.width}x{a.height} B={B} K0={k0.value} rounds={nr.value} lds={lds.value} "
       f"ms/launch={e0.elapsed_time(e1) / 5:.4f} waves={waves}")
 print("cycles per wave per round: " + ", ".join(f"{n} {v:.0f}" for n, v in per.items()))
+# per level: task cycles per builder wave per round (g_pstime[8 + l] over g_pstime[24 + l] waves)
+print("task cycles per round by level: " + ", ".join(
+    f"L{l} {out[8 + l] / max(out[24 + l], 1) / max(nr.value, 1):.0f} ({out[24 + l] // max(B * 5 + B, 1)} waves)"
+    for l in range(8) if out[24 + l]))
 print("cycles per wave total: " + ", ".join(f"{n} {out[i] / max(waves, 1):.0f}" for i, n in enumerate(names)))
 print("task cycles per wave per round by level: " + ", ".join(
     f"L{l} {out[8 + l] / max(out[24 + l], 1) / max(nr.value, 1):.0f}" for l in range(8) if out[24 + l]))

@@ -14,3 +14,9 @@ f = glob.glob("gpurun_out/r05_g/prof/**/*kernel_stats.csv", recursive=True)[0]
 for r in csv.DictReader(open(f)):
     print(r["Name"][:60], r["Calls"], round(float(r["AverageNs"]) / 1e3, 2), "us")
 PY
+timeout -k 10 120 python scripts/km_timing.py build/variants/km_t.so --per 2 || exit 1
+timeout -k 10 120 python scripts/km_timing.py build/variants/km_t.so --per 512 || exit 1
+#!/bin/bash
+set -o pipefail
+timeout -k 10 120 python scripts/ps_timing.py build/variants/ps_t.so --batch 512 || exit 1
+timeout -k 10 120 python scripts/ps_timing.py build/variants/ps_t.so --batch 512 --width 1241 --height 376 --nfeatures 2000 || exit 1
