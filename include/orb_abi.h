@@ -136,7 +136,8 @@ int orb_search_for_initialization(const orb_keypoint_t* kps1, const uint8_t* des
  * orb_extract_batch_device (d_kps / d_desc / d_counts with per-frame capacity `cap`).
  *   d_prev_xy: P x cap x 2 floats (in/out); NULL means "vbPrevMatched = F1 keypoints"
  *              (Tracking::FirstInitialization, reference Tracking.cc:366-368) and no update.
- *   d_matches12: P x cap int32; d_nmatches: P int32.  Asynchronous on `stream`.
+ *   d_matches12: P x cap int32; d_nmatches: P int32.  d_desc 16-B aligned.  Asynchronous on
+ *   `stream`.
  * cap <= 8192.  One workgroup per pair holds up to nmax octave-0 keypoints per frame in LDS:
  * nmax = min(cap, 1024) for P < 256 pairs, min(cap, 1024, max(256, ~9/40 cap)) otherwise (the
  * extractor keeps at most 0.217 nFeatures at level 0).  A pair over nmax (another producer, the
