@@ -86,6 +86,13 @@ __device__ __forceinline__ void glibc_sincosf(float y, float* s_out, float* c_ou
     *c_out = (n & 1) ? S : C;
 }
 
+// Minimum over each aligned group of 8 lanes (DPP: quad_perm xor 1, xor 2, row_half_mirror).
+__device__ __forceinline__ uint32_t min8(uint32_t v) {
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));
+    return min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false));
+}
+
 // DescriptorDistance (ORBmatcher.cc:1794-1810): popcount of the 256-bit XOR.
 __device__ __forceinline__ int hamming256(const uint32_t* a, const uint32_t* b) {
     int d = 0;

@@ -2412,12 +2412,6 @@ __device__ unsigned long long g_kmtime[8];
 #else
 #define KM_T(i)
 #endif
-// Minimum over each aligned group of 8 lanes (DPP: quad_perm xor 1, xor 2, row_half_mirror).
-__device__ __forceinline__ uint32_t min8(uint32_t v) {
-    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false));
-    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false));
-    return min(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false));
-}
 __device__ __forceinline__ void topk_insert(uint32_t (&t)[MATCH_TOPK], uint32_t key) {
 #pragma unroll
     for (int i = 0; i < MATCH_TOPK; ++i) {

@@ -44,6 +44,7 @@
 #include "orb_internal.h"
 
 using orbdev::hamming256;
+using orbdev::min8;
 
 namespace {
 
@@ -674,6 +675,31 @@ __device__ uint32_t triang_rescan(const Job& J, int q, const QP& p, const uint8_
     return wave_min(best);
 }
 
+// The acceptance test of each matcher for the query's best / second untaken candidates.
+template <int MODE>
+__device__ __forceinline__ bool accept_rule(const Job& J, int bestDist, int bestDist2, int bestLevel, int bestLevel2) {
+    switch (MODE) {
+        case M_LOCAL:  // 112-121
+            return bestDist <= TH_HIGH && !(bestLevel == bestLevel2 && (float)bestDist > J.nnratio * (float)bestDist2);
+        case M_WINDOW:  // 476
+        case M_F2F:     // 585
+            return (float)bestDist <= (float)bestDist2 * J.nnratio && bestDist <= TH_HIGH;
+        case M_BOW_KFF:  // 222-226
+            return bestDist <= TH_LOW && (float)bestDist < J.nnratio * (float)bestDist2;
+        case M_BOW_KFKF:  // 789-793
+            return bestDist < TH_LOW && (float)bestDist < J.nnratio * (float)bestDist2;
+        case M_MOTION:  // 1576
+            return bestDist <= TH_HIGH;
+        case M_RELOC:  // 1701
+        case M_SIM3P:  // 393
+            return bestDist <= J.thDist;
+        case M_TRIANG:
+            return true;
+        default:
+            return false;
+    }
+}
+
 // One instantiation per matcher (MODE == J.mode): the loop-carried pass of each is its own
 // straight-line code, without the other modes' branches.
 template <int MODE>
@@ -735,12 +761,13 @@ __global__ void __launch_bounds__(256) k_resolve(Job J) {
                 if (c + 1 < nch) load_chunk(c + 1, (c + 1) & 1);
             } else {
                 const int buf = c & 1, qend = min(RES_CHUNK, J.qn - c * RES_CHUNK);
-                for (int jq = 0; jq < qend; ++jq) {
+                // one query decided exactly (the triangulation walk, a query whose top-8 ran out)
+                auto single = [&](int jq) {
                     const int q = c * RES_CHUNK + jq;
                     const int2 fc = s_cq[buf][jq];
                     const int flags = __builtin_amdgcn_readfirstlane(fc.x), cnt = __builtin_amdgcn_readfirstlane(fc.y);
-                    if (!(flags & 1)) continue;
-                    if (cnt == 0) continue;
+                    if (!(flags & 1)) return;
+                    if (cnt == 0) return;
                     const uint32_t eL = lane < TOPK ? s_ce[buf][jq * TOPK + lane] : 0xFFFFFFFFu;
                     const uint32_t xL = lane < TOPK ? s_cx[buf][jq * TOPK + lane] : 0u;
                     const int k = min(cnt, TOPK);
@@ -771,7 +798,7 @@ __global__ void __launch_bounds__(256) k_resolve(Job J) {
                             decided = true;
                         }
                         if (!decided) chosen = triang_rescan(J, q, J.qp[q], s_taken, lane);
-                        if (chosen == 0xFFFFFFFFu) continue;
+                        if (chosen == 0xFFFFFFFFu) return;
                         bestIdx = key_idx(J, chosen);
                         bestDist = 0;  // accepted below unconditionally
                     } else {
@@ -802,7 +829,7 @@ __global__ void __launch_bounds__(256) k_resolve(Job J) {
                                 x2 = (uint32_t)i2x | ((uint32_t)J.T.kps[i2x].octave << 24);
                             }
                         }
-                        if (b1 == 0xFFFFFFFFu) continue;  // every candidate taken: bestDist stays INT_MAX
+                        if (b1 == 0xFFFFFFFFu) return;  // every candidate taken: bestDist stays INT_MAX
                         bestIdx = (int)(x1 & 0xFFFFFFu);
                         bestDist = (int)(b1 >> 16);
                         bestLevel = (int)(x1 >> 24);
@@ -811,36 +838,8 @@ __global__ void __launch_bounds__(256) k_resolve(Job J) {
                             bestLevel2 = (int)(x2 >> 24);
                         }
                     }
-                    bool accept = false;
-                    switch (m) {
-                        case M_LOCAL:  // 112-121
-                            accept = bestDist <= TH_HIGH &&
-                                     !(bestLevel == bestLevel2 && (float)bestDist > J.nnratio * (float)bestDist2);
-                            break;
-                        case M_WINDOW:  // 476
-                        case M_F2F:     // 585
-                            accept = (float)bestDist <= (float)bestDist2 * J.nnratio && bestDist <= TH_HIGH;
-                            break;
-                        case M_BOW_KFF:  // 222-226
-                            accept = bestDist <= TH_LOW && (float)bestDist < J.nnratio * (float)bestDist2;
-                            break;
-                        case M_BOW_KFKF:  // 789-793
-                            accept = bestDist < TH_LOW && (float)bestDist < J.nnratio * (float)bestDist2;
-                            break;
-                        case M_MOTION:  // 1576
-                            accept = bestDist <= TH_HIGH;
-                            break;
-                        case M_RELOC:  // 1701
-                        case M_SIM3P:  // 393
-                            accept = bestDist <= J.thDist;
-                            break;
-                        case M_TRIANG:
-                            accept = true;
-                            break;
-                        default:
-                            break;
-                    }
-                    if (!accept) continue;
+                    const bool accept = accept_rule<m>(J, bestDist, bestDist2, bestLevel, bestLevel2);
+                    if (!accept) return;
                     if (lane == 0) {
                         s_taken[bestIdx] = 1;
                         const int qv = qrow(J, q);
@@ -851,6 +850,78 @@ __global__ void __launch_bounds__(256) k_resolve(Job J) {
                     ++nacc;
                     // lane 0's LDS writes land before any lane's next read (same wave, in order)
                     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                };
+                if constexpr (m == M_TRIANG) {
+                    for (int jq = 0; jq < qend; ++jq) single(jq);
+                } else {
+                    // Speculated eight queries at a time (lane 8g + k: query jq + g, entry k of its
+                    // sorted top-8), as k_match_init's greedy pass: a query's outcome is fixed by its
+                    // first two untaken entries (best, second) and an acceptance takes exactly one
+                    // target, so every query of the batch is decided from the batch-start state
+                    // unless an earlier query of the batch accepted its best or second target, or it
+                    // needs the exact rescan (a truncated top-8 with too few untaken entries); the
+                    // batch commits its queries before the first such one.
+                    const int grp = lane >> 3, cand = lane & 7;
+                    const int need = needs_second(m) ? 2 : 1;
+                    int jq = 0;
+                    while (jq < qend) {
+                        const int nb = min(8, qend - jq);
+                        const int jg = jq + min(grp, nb - 1);
+                        const int2 fc = s_cq[buf][jg];
+                        const uint32_t eR = s_ce[buf][jg * TOPK + cand];
+                        const uint32_t xR = s_cx[buf][jg * TOPK + cand];
+                        const bool qok = grp < nb && (fc.x & 1) && fc.y > 0;
+                        const int cnt = qok ? fc.y : 0;
+                        const bool valid = cand < min(cnt, TOPK);
+                        const int idx = (int)(xR & 0xFFFFFFu);
+                        const bool untaken = valid && !s_taken[idx];
+                        const uint32_t best = min8(untaken ? eR : 0xFFFFFFFFu);
+                        const bool isB = untaken && eR == best;
+                        const uint32_t sec = min8(untaken && !isB ? eR : 0xFFFFFFFFu);
+                        const bool isS = untaken && eR == sec;
+                        // the targets (and octaves) of best and second, to every lane of the group
+                        const uint32_t tB = min8(isB ? xR : 0xFFFFFFFFu), tS = min8(isS ? xR : 0xFFFFFFFFu);
+                        const uint64_t um = __ballot(untaken);
+                        const int nUnt = __popcll((um >> (8 * grp)) & 0xFFull);
+                        const bool rescan = qok && cnt > TOPK && nUnt < need;
+                        bool accept = false;
+                        if (qok && !rescan && best != 0xFFFFFFFFu) {
+                            const int bestDist = (int)(best >> 16), bestLevel = (int)(tB >> 24);
+                            const int bestDist2 = sec != 0xFFFFFFFFu ? (int)(sec >> 16) : INT_MAX;
+                            const int bestLevel2 = sec != 0xFFFFFFFFu ? (int)(tS >> 24) : -1;
+                            accept = accept_rule<m>(J, bestDist, bestDist2, bestLevel, bestLevel2);
+                        }
+                        const int bIdx = (int)(tB & 0xFFFFFFu), sIdx = sec != 0xFFFFFFFFu ? (int)(tS & 0xFFFFFFu) : -1;
+                        // bit g: group g accepts
+                        const uint64_t accW = __ballot(accept && cand == 0);
+                        // lane 8g + k checks group k's accepted target against query g's best / second
+                        const int bIdxK = __shfl(bIdx, 8 * cand, 64);
+                        // (best-only matchers: the second does not decide, so only the best can be hit)
+                        const bool hit = cand < grp && ((accW >> (8 * cand)) & 1ull) &&
+                                         (bIdxK == bIdx || (need == 2 && bIdxK == sIdx));
+                        const uint64_t stopM = __ballot(grp < nb && (hit || (rescan && cand == 0)));
+                        const int jstop = stopM ? (__ffsll((unsigned long long)stopM) - 1) >> 3 : nb;
+                        if (accept && cand == 0 && grp < jstop) {
+                            // distinct targets (no hit before jstop): these writes commute
+                            s_taken[bIdx] = 1;
+                            const int qv = qrow(J, c * RES_CHUNK + jg);
+                            const int slot = J.outByTarget ? bIdx : qv;
+                            s_out[slot] = J.outByTarget ? qv : bIdx;
+                            if (rotMode) {
+                                // rank among the batch's committed acceptances: query order kept
+                                const uint64_t before = accW & ((1ull << (8 * grp)) - 1ull);
+                                s_acc[nacc + __popcll(before)] = slot << 5;
+                            }
+                        }
+                        nacc += __popcll(accW & (jstop >= 8 ? ~0ull : ((1ull << (8 * jstop)) - 1ull)));
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        if (jstop > 0) {
+                            jq += jstop;
+                        } else {
+                            single(jq);  // query jq needs the exact rescan
+                            jq += 1;
+                        }
+                    }
                 }
             }
             __syncthreads();  // chunk c decided, chunk c + 1 staged
