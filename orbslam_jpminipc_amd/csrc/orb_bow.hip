@@ -41,11 +41,7 @@ constexpr uint32_t NONE = 0xFFFFFFFFu;
 constexpr int BOW_WAVES = 16;  // waves per pair: the common nodes are dealt round-robin to them
 constexpr int BOW_T = 64 * BOW_WAVES;
 
-__device__ __forceinline__ uint32_t wmin(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
-    return v;
-}
+__device__ __forceinline__ uint32_t wmin(uint32_t v) { return orbdev::wave_min_u32(v); }
 
 __device__ __forceinline__ int rot_bin(float a1, float a2) {  // ORBmatcher.cc:230-236 / 799-805
     float rot = a1 - a2;

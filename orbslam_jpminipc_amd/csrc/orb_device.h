@@ -156,6 +156,16 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
 }
 // Sum over the 64 lanes, wave-uniform.
 __device__ __forceinline__ int wave_total(int v) { return __builtin_amdgcn_readlane(wave_incl_scan(v), 63); }
+// Minimum over the 64 lanes, wave-uniform: min8 (quad_perm, row_half_mirror), row_mirror, then
+// row_bcast:15 / row_bcast:31 across rows (an LDS-free butterfly; __shfl_xor pays six
+// ds_bpermute round trips).
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    v = min8(v);
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x140, 0xf, 0xf, false));  // row_mirror
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
 // The value of lane ^ 1.
 __device__ __forceinline__ int lane_xor1(int v) { return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, false); }
 

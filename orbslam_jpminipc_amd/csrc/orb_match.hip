@@ -192,16 +192,8 @@ __device__ __forceinline__ void load_desc(const uint32_t* p, uint32_t (&d)[8]) {
     const uint4 a = *(const uint4*)p, b = *(const uint4*)(p + 4);
     d[0] = a.x, d[1] = a.y, d[2] = a.z, d[3] = a.w, d[4] = b.x, d[5] = b.y, d[6] = b.z, d[7] = b.w;
 }
-__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
-    return v;
-}
-__device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) { return orbdev::wave_min_u32(v); }
+__device__ __forceinline__ int wave_sum(int v) { return orbdev::wave_total(v); }
 __device__ __forceinline__ void topk_insert(uint32_t (&t)[TOPK], uint32_t key) {
 #pragma unroll
     for (int i = 0; i < TOPK; ++i) {
@@ -783,13 +775,13 @@ __global__ void __launch_bounds__(256) k_resolve(Job J) {
                         bool decided = false;
                         if (um != 0ull) {
                             const int first = __ffsll((unsigned long long)um) - 1;
-                            const int distTh = 2 * (int)(__shfl(e, first, 64) >> 16);
+                            const int distTh = 2 * (int)((uint32_t)__builtin_amdgcn_readlane((int)e, first) >> 16);
                             const orb_keypoint_t kp1 = J.qkps[qrow(J, q)];
                             const bool inTh = lane < k && (int)(e >> 16) <= distTh;  // (epipolar: the target's point, below)
                             const bool pass = untaken && inTh && epipolar_ok(J, kp1, J.T.kps[eidx]);
                             const uint64_t pm = __ballot(pass), om = __ballot(lane < k && !inTh);
                             if (pm != 0ull) {
-                                chosen = __shfl(e, __ffsll((unsigned long long)pm) - 1, 64);
+                                chosen = (uint32_t)__builtin_amdgcn_readlane((int)e, __ffsll((unsigned long long)pm) - 1);
                                 decided = true;
                             } else if (om != 0ull || cnt <= TOPK) {
                                 decided = true;  // the walk breaks on an entry past DistTh, or ends

@@ -33,6 +33,7 @@
 #include <vector>
 
 #include "../../include/orb_abi.h"
+#include "orb_device.h"
 #include "orb_internal.h"
 
 namespace {
@@ -45,8 +46,8 @@ enum { kL1_NORM = 0, kL2_NORM = 1, kDOT_PRODUCT = 5 };
 
 struct VocDev {
     const uint4* slotDesc;     // child slot -> descriptor (2 x uint4)
-    const uint32_t* slotNode;  // child slot -> node id
-    const int2* nodeInfo;      // node -> {first child slot, number of children}
+    const uint4* slotInfo;     // child slot -> {node id, its first child slot, its number of children, 0}
+    int2 root;                 // the root's {first child slot, number of children}
     const uint32_t* wordId;    // node -> word id (0 for a non-word, as DBoW2's Node())
     const double* weight;      // node -> weight
     int maxDepth;              // tree height (bounds the descent)
@@ -69,7 +70,7 @@ __global__ void __launch_bounds__(256) k_voc_descend(VocDev V, const uint8_t* __
     const uint4 q0 = q[0], q1 = q[1];
     uint32_t node = 0, nodeAt = 0;  // nid_level <= 0 -> the root (TemplatedVocabulary.h:1227)
     bool set = nidLevel <= 0;
-    int2 inf = V.nodeInfo[0];
+    int2 inf = V.root;
     for (int level = 1;; ++level) {
         uint32_t best = 0xFFFFFFFFu;
         for (int j = sub; j < inf.y; j += VOC_GROUP) {
@@ -78,14 +79,17 @@ __global__ void __launch_bounds__(256) k_voc_descend(VocDev V, const uint8_t* __
                           __popc(q1.x ^ c.x) + __popc(q1.y ^ c.y) + __popc(q1.z ^ c.z) + __popc(q1.w ^ c.w);
             best = min(best, ((uint32_t)d << 16) | (uint32_t)j);
         }
-#pragma unroll
-        for (int o = VOC_GROUP / 2; o >= 1; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, VOC_GROUP));
-        node = V.slotNode[inf.x + (int)(best & 0xFFFFu)];
+        // min over the 16-lane group (a DPP row): no LDS round trip
+        best = orbdev::min8(best);
+        best = min(best, (uint32_t)__builtin_amdgcn_update_dpp((int)best, (int)best, 0x140, 0xf, 0xf, false));
+        // the chosen child's node and its children in one load (one dependent round trip per level)
+        const uint4 si = V.slotInfo[inf.x + (int)(best & 0xFFFFu)];
+        node = si.x;
         if (level == nidLevel) {
             nodeAt = node;
             set = true;
         }
-        inf = V.nodeInfo[node];
+        inf = make_int2((int)si.y, (int)si.z);
         if (inf.y == 0 || level >= V.maxDepth) break;  // isLeaf() (TemplatedVocabulary.h:1254)
     }
     if (sub == 0) {
@@ -252,8 +256,8 @@ struct orb_vocabulary {
     int k = 0, L = 0, scoring = 0, weighting = 0, device = 0;
     int nNodes = 0, nWords = 0, maxDepth = 0;
     uint4* d_slotDesc = nullptr;
-    uint32_t* d_slotNode = nullptr;
-    int2* d_nodeInfo = nullptr;
+    uint4* d_slotInfo = nullptr;
+    int2 rootInfo{0, 0};
     uint32_t* d_word = nullptr;
     double* d_weight = nullptr;
     // host entry point: own stream + scratch, one caller at a time
@@ -262,14 +266,13 @@ struct orb_vocabulary {
     uint8_t* d_scratch = nullptr;
     size_t scratchCap = 0;
 
-    VocDev dev() const { return VocDev{d_slotDesc, d_slotNode, d_nodeInfo, d_word, d_weight, maxDepth}; }
+    VocDev dev() const { return VocDev{d_slotDesc, d_slotInfo, rootInfo, d_word, d_weight, maxDepth}; }
 
     void release() {
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
         (void)hipFree(d_slotDesc);
-        (void)hipFree(d_slotNode);
-        (void)hipFree(d_nodeInfo);
+        (void)hipFree(d_slotInfo);
         (void)hipFree(d_word);
         (void)hipFree(d_weight);
         (void)hipFree(d_scratch);
@@ -302,18 +305,22 @@ struct orb_vocabulary {
             height = std::max(height, depth[i + 1]);
         }
         for (int v = 0; v < N; ++v) info[v] = make_int2(first[v], cnt[v]);
+        std::vector<uint4> sinfo(std::max(n, 1));
+        for (int s2 = 0; s2 < n; ++s2) {
+            const uint32_t nd = snode[s2];
+            sinfo[s2] = make_uint4(nd, (uint32_t)info[nd].x, (uint32_t)info[nd].y, 0u);
+        }
+        rootInfo = info[0];
         nNodes = N;
         nWords = words;
         maxDepth = std::max(height, 1);
         VCHK(hipSetDevice(device));
         VCHK(hipMalloc(&d_slotDesc, sdesc.size() * sizeof(uint4)));
-        VCHK(hipMalloc(&d_slotNode, snode.size() * 4));
-        VCHK(hipMalloc(&d_nodeInfo, (size_t)N * sizeof(int2)));
+        VCHK(hipMalloc(&d_slotInfo, sinfo.size() * sizeof(uint4)));
         VCHK(hipMalloc(&d_word, (size_t)N * 4));
         VCHK(hipMalloc(&d_weight, (size_t)N * 8));
         VCHK(hipMemcpy(d_slotDesc, sdesc.data(), sdesc.size() * sizeof(uint4), hipMemcpyHostToDevice));
-        VCHK(hipMemcpy(d_slotNode, snode.data(), snode.size() * 4, hipMemcpyHostToDevice));
-        VCHK(hipMemcpy(d_nodeInfo, info.data(), (size_t)N * sizeof(int2), hipMemcpyHostToDevice));
+        VCHK(hipMemcpy(d_slotInfo, sinfo.data(), sinfo.size() * sizeof(uint4), hipMemcpyHostToDevice));
         VCHK(hipMemcpy(d_word, wid.data(), (size_t)N * 4, hipMemcpyHostToDevice));
         VCHK(hipMemcpy(d_weight, wt.data(), (size_t)N * 8, hipMemcpyHostToDevice));
         VCHK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
