@@ -2761,11 +2761,9 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
                 }
             }
             uint32_t gb = lb;
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) gb = min(gb, (uint32_t)__shfl_xor((int)gb, o, 64));
+            gb = wave_min_u32(gb);
             int contrib = (lb == gb) ? ls : (lb == 0xFFFFFFFFu ? 0x7fffffff : (int)(lb >> KB));
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) contrib = min(contrib, __shfl_xor(contrib, o, 64));
+            contrib = (int)wave_min_u32((uint32_t)contrib);  // (non-negative)
             q0 += 1;
             if (gb == 0xFFFFFFFFu) continue;
             const int rDist = (int)(gb >> KB), rSlot = (int)(gb & SLOT);

@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "../../include/orb_abi.h"
+#include "orb_device.h"
 #include "orb_internal.h"
 
 namespace {
@@ -89,8 +90,7 @@ __global__ void __launch_bounds__(64) k_distinctive(const int32_t* __restrict__ 
         }
         best = min(best, ((uint32_t)lo << 16) | (uint32_t)i);
     }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, 64));
+    best = orbdev::wave_min_u32(best);
     const int bi = (int)(best & 0xFFFFu);
     if (lane == 0) bestRow[m] = s_rows[bi];
     if (lane < 8) ((uint32_t*)(outDesc + (size_t)m * 32))[lane] = s_d[(size_t)bi * 8 + lane];
