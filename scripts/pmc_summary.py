@@ -20,7 +20,8 @@ import json
 from collections import defaultdict
 
 
-WIDE_LOADS = {"k_pyr0", "k_pyr_stream", "k_pyr_resize", "k_fast", "k_orient_desc", "k_rerun"}  # k_rerun: round 4
+WIDE_LOADS = {"k_pyr0", "k_pyr_stream", "k_pyr_resize", "k_fast", "k_orient_desc", "k_rerun",  # k_rerun: round 4
+              "k_voc_descend", "k_bow_pairs"}  # round 5: 16-B child-descriptor / descriptor loads
 
 
 def main():
@@ -38,7 +39,7 @@ def main():
     acc = defaultdict(lambda: defaultdict(list))
     for f in sorted(glob.glob(f"{a.root}/p*/run_counter_collection.csv")):
         for r in csv.DictReader(open(f)):
-            name = r["Kernel_Name"].split("(")[0].split("<")[0].replace("void ", "")
+            name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].split("<")[0].replace("void ", "")
             acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
     mean = {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in acc.items()
             if not k.startswith("__amd") and "elementwise" not in k and "at::" not in k}
