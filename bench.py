@@ -405,7 +405,7 @@ def orbvoc_shaped_tree(k=10, L=6, seed=106):
     return parent, leaf, desc, weight
 
 
-def bow_leg(orb, d_kps, d_desc, d_cnt, f1, f2, steps, warmup, stream):
+def bow_leg(orb, d_kps, d_desc, d_cnt, f1, f2, steps, warmup, stream, workload=None, W=0, H=0, NF=0):
     """The BoW-bucketed matching path on the step's extractor output (north_star: "BoW-bucketed
     matching"): Frame::ComputeBoW for every frame (TemplatedVocabulary::transform with levelsup 4,
     Frame.cc:280-287) then SearchByBoW(KeyFrame = frame t, Frame = frame t+1) with
@@ -446,6 +446,12 @@ def bow_leg(orb, d_kps, d_desc, d_cnt, f1, f2, steps, warmup, stream):
     # match = both frames' descriptors read once + the output row (4 B per slot of frame b)
     b_tr = nfeat * (32 + 40)
     b_m = int(sum(32 * (cnt[a] + cnt[b]) + 4 * cap for a, b in zip(f1h, f2h)))
+    tr_pmc = m_pmc = None
+    if workload:
+        t1 = pmc_traffic("k_voc_descend", workload, W, H, B, NF)[0]
+        t2 = pmc_traffic("k_voc_bow", workload, W, H, B, NF)[0]
+        tr_pmc = t1 + t2 if t1 is not None and t2 is not None else None
+        m_pmc = pmc_traffic("k_bow_pairs", workload, W, H, B, NF)[0]
     return {
         "what": "Frame::ComputeBoW (transform, levelsup 4) on every frame + SearchByBoW(KF = frame t, F = frame t+1), "
                 "ORBmatcher(0.7, true), batched on the device",
@@ -456,9 +462,12 @@ def bow_leg(orb, d_kps, d_desc, d_cnt, f1, f2, steps, warmup, stream):
         "matches_per_pair": float(nm_h.mean()),
         "transform_roofline": {"bound": "hbm", "achieved": b_tr / (t_tr * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                                "unit": "GB/s", "frac": b_tr / (t_tr * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                               "algorithmic_bytes": b_tr},
+                               "algorithmic_bytes": b_tr, "traffic": tr_pmc, "traffic_kernels": "k_voc_descend + k_voc_bow",
+                               "traffic_unit": "bytes per step (rocprofv3 PMC, profiles/pmc_<workload>.json)"},
         "match_roofline": {"bound": "hbm", "achieved": b_m / (t_m * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-                           "unit": "GB/s", "frac": b_m / (t_m * 1e-3) / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes": b_m},
+                           "unit": "GB/s", "frac": b_m / (t_m * 1e-3) / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes": b_m,
+                           "traffic": m_pmc, "traffic_kernels": "k_bow_pairs",
+                           "traffic_unit": "bytes per launch (rocprofv3 PMC, profiles/pmc_<workload>.json)"},
     }
 
 
@@ -908,7 +917,7 @@ def run_rank(args):
         hf["vs_device_resident"] = hf["value"] / value
         result["host_fed"] = hf
     if rank == 0 and world == 1 and args.bow:
-        result["bow"] = bow_leg(orb, d_kps, d_desc, d_cnt, f1, f2, 10, 3, s_ext)
+        result["bow"] = bow_leg(orb, d_kps, d_desc, d_cnt, f1, f2, 10, 3, s_ext, args.workload, W, H, NF)
     if rank == 0 and world == 1 and args.latency:
         result["latency_b1"] = latency_b1(orb, W, H, NF, local, frames[:2])
     if rank == 0 and world == 1 and args.cpu_frames > 0:
