@@ -68,6 +68,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md §Chip-level par
 N_CU, CLOCK_HZ = 256, 2.4e9
 SALU_PEAK = N_CU * CLOCK_HZ  # SALU instructions / s: one scalar unit per CU, one issue per cycle
 LDS_PEAK = N_CU * CLOCK_HZ   # LDS pipe cycles / s: one per CU per cycle
+# Measured VALU issue rate of the 4-cycle instruction kinds (v_perm, v_pk_*, v_alignbyte, v_bfe,
+# v_dot*, v_mul_*24, v_min/max_u32, DPP moves, 3-source VOP3) with 8 waves per SIMD, all CUs busy:
+# 0.58 wave64 instructions per ns per SIMD (scripts/valu_rate.hip, profiles/r05_valu_rate.json;
+# add / and / or / shift / f32 fma reach 1.08 alone, but a 1:1 mix with a 4-cycle kind runs 0.61)
+VALU_4C_PEAK = N_CU * 4 * 0.58e9
 METRIC = "frames/sec ORB extract+match, 640x480 8-level 1000 kp; HBM GB/s vs peak"
 
 WORKLOADS = {
@@ -824,6 +829,9 @@ def run_rank(args):
     launch_s = ds["ms_per_launch"] * 1e-3
     if valu_insts:
         roofs["valu_issue"] = valu_insts / launch_s / valu_peak
+        # the same instructions against the measured issue rate of the instruction kinds these
+        # kernels are made of (4 cycles per wave64 instruction): the practical VALU ceiling
+        roofs["valu_issue_4c"] = valu_insts / launch_s / VALU_4C_PEAK
     salu_insts = pmc.get("SQ_INSTS_SALU")
     if salu_insts:
         # one scalar unit per CU issuing one SALU instruction per cycle (MI355X_MICROARCH.md: 4
@@ -882,6 +890,7 @@ def run_rank(args):
             "algorithmic_bytes_basis": "SURVEY.md §8d, this stage's terms only (bench.stage_bytes)",
             "valu_insts_per_launch": valu_insts,
             "valu_issue_frac": roofs.get("valu_issue"),
+            "valu_issue_4c_frac": roofs.get("valu_issue_4c"),
             "salu_issue_frac": roofs.get("salu_issue"),
             "lds_issue_frac": roofs.get("lds_issue"),
             # the other issue ports of the same PMC pass: SALU (one per CU per cycle) and the LDS
@@ -894,7 +903,9 @@ def run_rank(args):
             "roofs": roofs,
             "bound_note": "bound/frac price the kernel against the HBM roofline with SURVEY §8d algorithmic "
                           "bytes (the contract's figure); `binding` names the roof that limits it, from the "
-                          "same PMC pass: valu_issue = SQ_INSTS_VALU / (1024 SIMDs x 1 per 2 cycles), "
+                          "same PMC pass: valu_issue = SQ_INSTS_VALU / (1024 SIMDs x 1 per 2 cycles), valu_issue_4c = "
+                          "SQ_INSTS_VALU / (1024 SIMDs x 0.58 per ns, the measured rate of the 4-cycle "
+                          "instruction kinds, profiles/r05_valu_rate.json), "
                           "salu_issue = SQ_INSTS_SALU / (256 CUs x 1 per cycle), lds_issue = (SQ_INSTS_LDS "
                           "+ SQ_LDS_BANK_CONFLICT) / (256 CUs x 1 per cycle), hbm_measured_traffic = PMC "
                           "bytes / 8 TB/s; all at 2.4 GHz over the event-timed launch",

@@ -151,10 +151,14 @@ using namespace orbdev;
 
 __constant__ signed char c_pattern[1024];
 __constant__ float c_patternf[1024];  // the same pattern as floats: lane l's 8 points are 4 float4
-// IC_Angle disc masks (ORBextractor.cc:124-151 with umax, 495-510) of the 31 x 9 patch dwords for
-// each byte alignment sh of the patch in its dword row: byte i of dword n = 9 r + c is inside the
-// disc iff |4c + i - sh - 15| <= umax[|r - 15|]
-__constant__ uint32_t c_icmask[4 * 320];
+// IC_Angle (ORBextractor.cc:124-151 with umax, 495-510) over the 31 x 9 patch dwords n = 9 r + c
+// (five 64-lane steps, n < 320; n >= 279 carry zero coefficients): c_icoff[n] = the dword's byte
+// offset in k_orient_desc's window from the patch's first dword; per byte alignment sh of the
+// patch in its dword row, c_ic10 / c_ic01[320 sh + n] = the signed byte coefficients u = 4c + i -
+// sh - 15 / v = r - 15 of byte i where it lies inside the disc (|u| <= umax[|v|]), else 0
+__constant__ uint32_t c_icoff[320];
+__constant__ uint32_t c_ic10[4 * 320];
+__constant__ uint32_t c_ic01[4 * 320];
 // k_orient_desc's row-pass B fragments: [N-tile t][lane l] = bytes j of B[16(l >> 4) + j][16t + (l & 15)]
 __constant__ uint4 c_rowB[4 * 64];  // 279 patch dwords per alignment, zero-padded to 5 x 64
 // ---- pyramid --------------------------------------------------------------------------
@@ -2145,7 +2149,7 @@ __global__ void __launch_bounds__(64 * OD_WAVES) k_orient_desc(const uint8_t* __
     const uint32_t pu = (uint32_t)lg.pitch >> 4;
     uint8_t* W = s_buf[wave];
     uint32_t* Hs = (uint32_t*)s_buf[wave];
-    uint32_t icm[5];  // IC_Angle disc masks of the patch dwords this lane reads
+    uint32_t ico[5], ic10[5], ic01[5];  // IC_Angle: the lane's patch dwords and their coefficients
     i32x4v Bf[4];  // the row pass's B fragments (constant; in flight with the window loads)
     // (PC-relative addresses per table load: routing the tables through one opaque SGPR base
     // saved ~30 SALU per wave but let the loads sink below the window's, 0.420 -> 0.440 ms c3)
@@ -2158,40 +2162,44 @@ __global__ void __launch_bounds__(64 * OD_WAVES) k_orient_desc(const uint8_t* __
         const int i = lane + 64 * j, r = i >> 2, c = i & 3;
         v[j] = src[i < NU ? __umul24((uint32_t)r, pu) + c : 0u];
     }
-    // the IC disc masks of this alignment, in flight with the window
+    // the IC tables of this alignment (dword loads), in flight with the window
 #pragma unroll
-    for (int j = 0; j < 5; ++j) icm[j] = c_icmask[320 * ((x + 1 - xa) & 3) + lane + 64 * j];
+    for (int j = 0; j < 5; ++j) {
+        const int sh320 = 320 * ((x + 1 - xa) & 3);
+        ico[j] = c_icoff[lane + 64 * j];
+        ic10[j] = c_ic10[sh320 + lane + 64 * j];
+        ic01[j] = c_ic01[sh320 + lane + 64 * j];
+    }
     {
-        // all 192 units stored (units >= 172 repeat unit 0 into the buffer's unused tail,
-        // before the row-pass sums are written): no masked store
+        // the window as i8 p - 128 (p ^ 0x80): the row pass's MFMA operand as it is, and IC_Angle's
+        // sums unchanged (the disc is symmetric in u and v: sum u = sum v = 0 over it).  All 192
+        // units stored (units >= 172 repeat unit 0 into the buffer's unused tail, before the
+        // row-pass sums are written): no masked store
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
             const int i = lane + 64 * j;
-            ((uint4*)W)[(i >> 2) * (OD_WP / 16) + (i & 3)] = v[j];
+            const uint4 w = make_uint4(v[j].x ^ 0x80808080u, v[j].y ^ 0x80808080u, v[j].z ^ 0x80808080u,
+                                       v[j].w ^ 0x80808080u);
+            ((uint4*)W)[(i >> 2) * (OD_WP / 16) + (i & 3)] = w;
         }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // LDS is in order per wave; compiler fence
     // IC_Angle (ORBextractor.cc:124-151): the disc sums m10 = sum u*I, m01 = sum v*I over
     // |u| <= umax[|v|], one patch dword per lane and step (patch row v = window row v + 21,
-    // patch dword c = window dword pd0 + c).  Byte i of dword c sits at u = base + i,
-    // base = 4c - sh - 15, so a dword adds base * S + sum(i * I_i) to m10 and v * S to m01,
-    // S = its in-disc byte sum: two v_dot4 on the masked dword (integer sums: any order).
+    // patch dword c = window dword pd0 + c): two v_dot4_i32_i8 of the window dword (p - 128)
+    // with the dword's coefficient bytes (0 outside the disc).  sum u (p - 128) = sum u p since
+    // sum u = 0 over the symmetric disc (likewise v): exact integer sums, any order.
     int m01 = 0, m10 = 0;
     {
         const int pc = x + 1 - xa;  // window column of patch column u = -15
-        const int pd0 = pc >> 2, sh = pc & 3;
-        const uint32_t* W32 = (const uint32_t*)W;
+        const uint8_t* P0 = W + (OD_WR - HALF_PATCH) * OD_WP + 4 * (pc >> 2);  // the patch's first dword
         // five full 64-lane steps: dwords n >= 279 (patch rows 31 .. 35, still inside the
-        // 43-row window) carry zero masks, so no lane is masked off
+        // 43-row window) carry zero coefficients, so no lane is masked off
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
-            const int n = lane + 64 * j;
-            const int r = n / 9, c = n - r * 9;
-            const uint32_t pm = W32[(r + OD_WR - HALF_PATCH) * (OD_WP / 4) + pd0 + c] & icm[j];
-            const int S = (int)__builtin_amdgcn_udot4(pm, 0x01010101u, 0u, false);
-            const int T = (int)__builtin_amdgcn_udot4(pm, 0x03020100u, 0u, false);
-            m10 += __mul24(4 * c - sh - HALF_PATCH, S) + T;  // 24-bit multiplies: full-rate VALU
-            m01 += __mul24(r - HALF_PATCH, S);
+            const int pm = *(const int*)(P0 + ico[j]);
+            m10 = __builtin_amdgcn_sdot4(pm, (int)ic10[j], m10, false);
+            m01 = __builtin_amdgcn_sdot4(pm, (int)ic01[j], m01, false);
         }
     }
     // output position: level-major order (ORBextractor.cc:749-778)
@@ -2237,10 +2245,10 @@ __global__ void __launch_bounds__(64 * OD_WAVES) k_orient_desc(const uint8_t* __
 #pragma unroll
         for (int m = 0; m < 3; ++m) {
             i32x4v a;
-            a.x = (int)(A[m].x ^ 0x80808080u);
-            a.y = (int)(A[m].y ^ 0x80808080u);
-            a.z = (int)(A[m].z ^ 0x80808080u);
-            a.w = (int)(((A[m].w ^ 0x80808080u) & keep) | bias);
+            a.x = (int)A[m].x;  // the window is stored as p ^ 0x80
+            a.y = (int)A[m].y;
+            a.z = (int)A[m].z;
+            a.w = (int)((A[m].w & keep) | bias);
             i32x4v c[4];
 #pragma unroll
             for (int t = 0; t < 4; ++t) c[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a, Bf[t], zero, 0, 0, 0);
@@ -3849,16 +3857,25 @@ static int upload_pattern(int device) {
             um[v] = v0;
             ++v0;
         }
-        uint32_t mt[4 * 320] = {};
+        uint32_t off[320], c10[4 * 320] = {}, c01[4 * 320] = {};
+        for (int n = 0; n < 320; ++n) off[n] = (uint32_t)(OD_WP * (n / 9) + 4 * (n % 9));
         for (int sh = 0; sh < 4; ++sh)
             for (int n = 0; n < 31 * 9; ++n) {
                 const int r = n / 9, c = n % 9, v = std::abs(r - 15);
-                uint32_t m = 0;
-                for (int i = 0; i < 4; ++i)
-                    if (std::abs(4 * c + i - sh - 15) <= um[v]) m |= 0xFFu << (8 * i);
-                mt[320 * sh + n] = m;
+                uint32_t w10 = 0, w01 = 0;
+                for (int i = 0; i < 4; ++i) {
+                    const int u = 4 * c + i - sh - 15;
+                    if (std::abs(u) <= um[v]) {
+                        w10 |= (uint32_t)(uint8_t)(int8_t)u << (8 * i);
+                        w01 |= (uint32_t)(uint8_t)(int8_t)(r - 15) << (8 * i);
+                    }
+                }
+                c10[320 * sh + n] = w10;
+                c01[320 * sh + n] = w01;
             }
-        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_icmask), mt, sizeof(mt)));
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_icoff), off, sizeof(off)));
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_ic10), c10, sizeof(c10)));
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_ic01), c01, sizeof(c01)));
     }
     {  // banded 7-tap row-pass matrix (GaussianBlur 7x7 sigma 2 fixed-point taps) + the bias rows
         static const int8_t tap[7] = {18, 34, 49, 55, 49, 34, 18};
