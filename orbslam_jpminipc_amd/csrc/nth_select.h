@@ -186,10 +186,14 @@ ORB_HD inline int retain_best(T* a, int n, int keep, Greater comp) {
 // cursor stops on the element the previous swap put there).  Positions in the untouched middle
 // keep their original values, so the stopper lists of the original array decide everything:
 // ballot-compacted lists, a ballot count of K, disjoint swaps.
+// set bits of a ballot mask below the calling lane (v_mbcnt_lo / v_mbcnt_hi)
+__device__ inline int lanes_below_wave(uint64_t m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 template <class T, class Greater>
 __device__ inline int unguarded_partition_wave(T* a, int lo, int hi, T pv, Greater comp, uint16_t* Lp, uint16_t* Rp,
                                                int lane) {
-    const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     int nl = 0, nr = 0;
     for (int c0 = lo; c0 < hi; c0 += 64) {
         const int p = c0 + lane;
@@ -200,8 +204,8 @@ __device__ inline int unguarded_partition_wave(T* a, int lo, int hi, T pv, Great
             rs = !comp(pv, v);
         }
         const uint64_t mL = __ballot(ls), mR = __ballot(rs);
-        if (ls) Lp[nl + __popcll(mL & below)] = (uint16_t)p;
-        if (rs) Rp[nr + __popcll(mR & below)] = (uint16_t)p;
+        if (ls) Lp[nl + lanes_below_wave(mL)] = (uint16_t)p;
+        if (rs) Rp[nr + lanes_below_wave(mR)] = (uint16_t)p;
         nl += __popcll(mL);
         nr += __popcll(mR);
     }

@@ -156,6 +156,12 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
 }
 // Sum over the 64 lanes, wave-uniform.
 __device__ __forceinline__ int wave_total(int v) { return __builtin_amdgcn_readlane(wave_incl_scan(v), 63); }
+// Set bits of a ballot mask below the calling lane: the lane's slot in a ballot-compacted append
+// (v_mbcnt_lo / v_mbcnt_hi on the mask's SGPR halves; popcount(m & lanes-below mask) took two
+// v_and and two v_bcnt on a per-lane VGPR mask)
+__device__ __forceinline__ int lanes_below(uint64_t m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
 // Minimum over the 64 lanes, wave-uniform: min8 (quad_perm, row_half_mirror), row_mirror, then
 // row_bcast:15 / row_bcast:31 across rows (an LDS-free butterfly; __shfl_xor pays six
 // ds_bpermute round trips).

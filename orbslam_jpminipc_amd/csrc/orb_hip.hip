@@ -842,35 +842,38 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
 typedef short i16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
-// Compass pre-filter of cv::FAST for the 4 pixels of a dword, in packed 16-bit arithmetic:
-// even and odd bytes are split into u16 pairs.  Bright: (q0 > v+t or q8 > v+t) and (q4 or q12
-// likewise) <=> min(max(q0, q8), max(q4, q12)) > v + t; dark: max(min(q0, q8), min(q4, q12))
-// < v - t; each comparison is the sign of an i16 difference (all values within i16).
+// Compass pre-filter of cv::FAST for the 4 pixels of a dword, in packed 16-bit arithmetic on
+// the dword's even and odd bytes (pixels x, x+2 / x+1, x+3) split into u16 lanes by the caller.
+// Bright: (q0 > v+t or q8 > v+t) and (q4 or q12 likewise) <=> M = min(max(q0, q8), max(q4, q12))
+// > v + t; dark: m = max(min(q0, q8), min(q4, q12)) < v - t; so the pixel passes <=>
+// max(M - v, v - m) > t, the sign of t - max(M - v, v - m) (all values within i16).
 // Returns a 4-bit mask (bit j = pixel j passes).
-__device__ __forceinline__ uint32_t compass4(uint32_t c, uint32_t q0, uint32_t q4, uint32_t q8, uint32_t q12,
-                                             uint32_t tt) {
-    uint32_t pass[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const uint32_t sel = h ? 0x0c030c01u : 0x0c020c00u;  // odd / even bytes -> u16 lanes
-        const i16x2 v = __builtin_bit_cast(i16x2, __builtin_amdgcn_perm(0u, c, sel));
-        const u16x2 a = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(0u, q0, sel));
-        const u16x2 b = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(0u, q4, sel));
-        const u16x2 d = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(0u, q8, sel));
-        const u16x2 e = __builtin_bit_cast(u16x2, __builtin_amdgcn_perm(0u, q12, sel));
-        const i16x2 t = __builtin_bit_cast(i16x2, tt);
-        const i16x2 M = __builtin_bit_cast(
-            i16x2, __builtin_elementwise_min(__builtin_elementwise_max(a, d), __builtin_elementwise_max(b, e)));
-        const i16x2 m = __builtin_bit_cast(
-            i16x2, __builtin_elementwise_max(__builtin_elementwise_min(a, d), __builtin_elementwise_min(b, e)));
-        const uint32_t br = __builtin_bit_cast(uint32_t, (i16x2)((v + t) - M));  // < 0: bright
-        const uint32_t dk = __builtin_bit_cast(uint32_t, (i16x2)(m - (v - t)));  // < 0: dark
-        pass[h] = (br | dk) & 0x80008000u;
-    }
+__device__ __forceinline__ uint32_t compass_half(uint32_t v, uint32_t q0, uint32_t q4, uint32_t q8, uint32_t q12,
+                                                 uint32_t tt) {
+    const u16x2 a = __builtin_bit_cast(u16x2, q0), b = __builtin_bit_cast(u16x2, q4);
+    const u16x2 d = __builtin_bit_cast(u16x2, q8), e = __builtin_bit_cast(u16x2, q12);
+    const i16x2 M = __builtin_bit_cast(
+        i16x2, __builtin_elementwise_min(__builtin_elementwise_max(a, d), __builtin_elementwise_max(b, e)));
+    const i16x2 m = __builtin_bit_cast(
+        i16x2, __builtin_elementwise_max(__builtin_elementwise_min(a, d), __builtin_elementwise_min(b, e)));
+    const i16x2 vv = __builtin_bit_cast(i16x2, v);
+    const i16x2 X = __builtin_elementwise_max((i16x2)(M - vv), (i16x2)(vv - m));
+    return __builtin_bit_cast(uint32_t, (i16x2)(__builtin_bit_cast(i16x2, tt) - X));  // bit 15 / 31: passes
+}
+__device__ __forceinline__ uint32_t compass_mask(uint32_t pe, uint32_t po) {
     // bit 15 / 31 of even -> pixels 0 / 2, of odd -> pixels 1 / 3: bytes (even 1, odd 1, even 3,
     // odd 3) gathered by one v_perm, their sign bits to bit 0 of each byte, packed by one v_dot4
-    const uint32_t g4 = (__builtin_amdgcn_perm(pass[1], pass[0], 0x07030501u) >> 7) & 0x01010101u;
+    const uint32_t g4 = (__builtin_amdgcn_perm(po, pe, 0x07030501u) >> 7) & 0x01010101u;
     return __builtin_amdgcn_udot4(g4, 0x08040201u, 0u, false);
+}
+__device__ __forceinline__ uint32_t even_bytes(uint32_t w) { return __builtin_amdgcn_perm(0u, w, 0x0c020c00u); }
+__device__ __forceinline__ uint32_t odd_bytes(uint32_t w) { return __builtin_amdgcn_perm(0u, w, 0x0c030c01u); }
+// the pre-filter of one dword from its five words (centre, q0 = 3 rows below, q4 = 3 px right,
+// q8 = 3 rows above, q12 = 3 px left)
+__device__ __forceinline__ uint32_t compass4(uint32_t c, uint32_t q0, uint32_t q4, uint32_t q8, uint32_t q12,
+                                             uint32_t tt) {
+    return compass_mask(compass_half(even_bytes(c), even_bytes(q0), even_bytes(q4), even_bytes(q8), even_bytes(q12), tt),
+                        compass_half(odd_bytes(c), odd_bytes(q0), odd_bytes(q4), odd_bytes(q8), odd_bytes(q12), tt));
 }
 
 // ---- FAST strength --------------------------------------------------------------------------
@@ -1032,7 +1035,6 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
         uint32_t* q = (uint32_t*)(In + inW * (dh + 6)) + 4 + wave * (RR_Q + 8);  // after the staged ROI
         // i / d = umulhi(i, ceil(2^32 / d)) for d >= 2 (the reciprocal of 1 does not fit 32 bits)
         const uint32_t m = (uint32_t)((0x100000000ull + dw - 1) / (uint64_t)dw);
-        const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
         // staged dword columns holding detection pixels: In byte c = xx + 3 + o, xx in [0, dw)
         const int wd0 = (3 + o) >> 2, nd = ((dw + 2 + o) >> 2) - wd0 + 1;
         const uint32_t md = (uint32_t)((0x100000000ull + nd - 1) / (uint64_t)nd);
@@ -1070,7 +1072,7 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
                 for (int j = 0; j < 4; ++j) {
                     const bool c = (mask >> j) & 1u;
                     const uint64_t bm = __ballot(c);
-                    q[c ? np + __popcll(bm & below) : RR_Q] = (uint32_t)(px0 + j);  // RR_Q: trash slot
+                    q[c ? np + lanes_below(bm) : RR_Q] = (uint32_t)(px0 + j);  // RR_Q: trash slot
                     np += __popcll(bm);
                 }
             }
@@ -1094,7 +1096,6 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
     // (LDS atomics); the per-word pass below turns the masks into raster-order records
     {
         uint32_t* q = (uint32_t*)(In + inW * (dh + 6)) + 4 + wave * (RR_Q + 8);
-        const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
         const uint32_t* Sp32 = (const uint32_t*)Sp;
         const uint32_t mr = rw > 1 ? (uint32_t)((0x100000000ull + rw - 1) / (uint64_t)rw) : 0u;
         auto nms = [&](int n) {
@@ -1133,7 +1134,7 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
             for (int j = 0; j < 4; ++j) {
                 const bool v = ((w4 >> (8 * j)) & 0xFFu) != 0u;
                 const uint64_t m = __ballot(v);
-                q[v ? cn + __popcll(m & below) : RR_Q] = ((uint32_t)yy << 16) | (uint32_t)(4 * wd + j);
+                q[v ? cn + lanes_below(m) : RR_Q] = ((uint32_t)yy << 16) | (uint32_t)(4 * wd + j);
                 cn += __popcll(m);
             }
             if (cn > RR_Q - 256) {
@@ -1776,7 +1777,6 @@ __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, G
     KF_T(1);
     const int ft = g.fastTh;
     const uint32_t tt = (uint32_t)ft | ((uint32_t)ft << 16);
-    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint16_t* pq = s_q[wave];
     uint16_t* px = s_px[wave];
     // pixel code = plane row << 9 | plane column (plane row = tile row + 1, plane column = tile
@@ -1798,7 +1798,7 @@ __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, G
         }
         const uint64_t m = __ballot(corner);
         if (corner) {
-            const int ix = ncl + __popcll(m & below);
+            const int ix = ncl + lanes_below(m);
             cl[ix < g.fastCl ? ix : FT_CL] = code;  // FT_CL: trash slot
         }
         ncl += __popcll(m);
@@ -1817,7 +1817,7 @@ __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, G
             for (int j = 0; j < 4; ++j) {  // expand the 64 entries into one pixel per slot
                 const bool v = (e >> j) & 1u;
                 const uint64_t m = __ballot(v);
-                px[v ? np + __popcll(m & below) : FT_CQ] = (uint16_t)(code + j);
+                px[v ? np + lanes_below(m) : FT_CQ] = (uint16_t)(code + j);
                 np += __popcll(m);
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1859,15 +1859,28 @@ __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, G
             uint32_t h[KF_DPL + 2];  // dwords -1 .. KF_DPL of the group's row
 #pragma unroll
             for (int j = 0; j < KF_DPL + 2; ++j) h[j] = row[j - 1];
-            const int dc = valid ? KF_DPL * kp : 0;
+            const int dc = valid ? KF_DPL * kp : fw;  // s_cm[fw ..] = 0: nothing queued
             const int fq = pr * fw + KF_DPL * kp;
+            // the row's dwords split once into even / odd byte lanes: a dword's q4 / q12 (pixels
+            // x+3 / x-3) are the odd / even lanes of its neighbours, one v_alignbyte where they
+            // straddle two dwords
+            uint32_t he[KF_DPL + 2], ho[KF_DPL + 2];
+#pragma unroll
+            for (int j = 0; j < KF_DPL + 2; ++j) {
+                he[j] = even_bytes(h[j]);
+                ho[j] = odd_bytes(h[j]);
+            }
             uint32_t m[KF_DPL];
 #pragma unroll
             for (int j = 0; j < KF_DPL; ++j) {
                 const uint32_t up = row[j - 3 * iw], dn = row[j + 3 * iw];
-                m[j] = compass4(h[j + 1], dn, __builtin_amdgcn_alignbyte(h[j + 2], h[j + 1], 3), up,
-                                __builtin_amdgcn_alignbyte(h[j + 1], h[j], 1), tt) & s_cm[dc + j];
-                m[j] = valid ? m[j] : 0u;
+                // even lanes (x, x+2): q4 = x+3, x+5 (odd bytes 3 / 1 of dwords 0 / +1), q12 = x-3, x-1
+                const uint32_t pe = compass_half(he[j + 1], even_bytes(dn), __builtin_amdgcn_alignbyte(ho[j + 2], ho[j + 1], 2),
+                                                 even_bytes(up), ho[j], tt);
+                // odd lanes (x+1, x+3): q4 = x+4, x+6 (even bytes of +1), q12 = x-2, x (bytes 2 / 0 of -1 / 0)
+                const uint32_t po = compass_half(ho[j + 1], odd_bytes(dn), he[j + 2], odd_bytes(up),
+                                                 __builtin_amdgcn_alignbyte(he[j + 1], he[j], 2), tt);
+                m[j] = compass_mask(pe, po) & s_cm[dc + j];
             }
             g += 256;
             kp += r256;
@@ -1886,7 +1899,7 @@ __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, G
             for (int j = 0; j < KF_DPL; ++j) {
                 const bool v = m[j] != 0u;
                 const uint64_t bm = __ballot(v);
-                pq[v ? qn + __popcll(bm & below) : FT_Q] = (uint16_t)(((uint32_t)(fq + j) << 4) | m[j]);
+                pq[v ? qn + lanes_below(bm) : FT_Q] = (uint16_t)(((uint32_t)(fq + j) << 4) | m[j]);
                 qn += (int)__popcll(bm);
             }
         }
@@ -1946,7 +1959,7 @@ __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, G
             }
             // survivors overwrite the front of the list (k0 + 64 > sn: no unread entry is hit)
             const uint64_t m = __ballot(keep);
-            pq[keep ? sn + __popcll(m & below) : FT_Q] = e;
+            pq[keep ? sn + lanes_below(m) : FT_Q] = e;
             sn += __popcll(m);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1985,7 +1998,7 @@ __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, G
             for (int j = 0; j < 4; ++j) {
                 const bool v = ((w4 >> (8 * j)) & 0xFFu) != 0u;
                 const uint64_t m = __ballot(v);
-                pq[v ? cn + __popcll(m & below) : FT_Q] = (uint16_t)((r << 9) | (4 * d + j));
+                pq[v ? cn + lanes_below(m) : FT_Q] = (uint16_t)((r << 9) | (4 * d + j));
                 cn += __popcll(m);
             }
             if (cn > FT_Q - 256) {
@@ -2514,7 +2527,6 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
     }
     uint32_t* s_key = s_list;  // phase-0 scratch (cap entries)
     KM_T(0);
-    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     // ---- phase 0: keys in parallel, then ordered compaction ----
     // s_key[i2] = traversal key of F2 keypoint i2 or ~0 (not octave 0 / outside the grid);
     // s_m12[i1] = 1 if F1 keypoint i1 is a query (octave 0), as scratch.
@@ -2534,7 +2546,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
             const uint32_t key = i0 + lane < n2 ? s_key[i0 + lane] : 0xFFFFFFFFu;
             const bool ok = key != 0xFFFFFFFFu;
             const uint64_t m = __ballot(ok);
-            if (ok) s_key[base + __popcll(m & below)] = key;
+            if (ok) s_key[base + lanes_below(m)] = key;
             base += __popcll(m);
         }
         if (lane == 0) s_n2c = base;
@@ -2544,7 +2556,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
             const int i1 = i0 + lane;
             const bool ok = i1 < n1 && s_m12[i1];
             const uint64_t m = __ballot(ok);
-            if (ok && base + __popcll(m & below) < nmax) s_q2i[base + __popcll(m & below)] = i1;
+            if (ok && base + lanes_below(m) < nmax) s_q2i[base + lanes_below(m)] = i1;
             base += __popcll(m);
         }
         if (lane == 0) s_n1c = base;

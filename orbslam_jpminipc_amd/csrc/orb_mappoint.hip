@@ -45,7 +45,6 @@ __global__ void __launch_bounds__(64) k_distinctive(const int32_t* __restrict__ 
     const int r0 = offsets[m], r1 = offsets[m + 1];
     const int cap = r1 - r0;
     int* s_rows = (int*)(s_d + (size_t)cap * 8);
-    const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     // vDescriptors: the usable observations, in order (MapPoint.cc:204-210)
     int N = 0;
     for (int c0 = 0; c0 < cap; c0 += 64) {
@@ -53,7 +52,7 @@ __global__ void __launch_bounds__(64) k_distinctive(const int32_t* __restrict__ 
         const bool ok = c0 + lane < cap && (!usable || usable[r]);
         const uint64_t msk = __ballot(ok);
         if (ok) {
-            const int pos = N + __popcll(msk & below);
+            const int pos = N + orbdev::lanes_below(msk);
             s_rows[pos] = r;
             const uint4* src = (const uint4*)(desc + (size_t)r * 32);
             uint4* dst = (uint4*)(s_d + (size_t)pos * 8);

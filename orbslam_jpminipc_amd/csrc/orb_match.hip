@@ -553,7 +553,6 @@ __global__ void __launch_bounds__(256) k_area_fill(Job J) {
     if (q >= J.qn) return;
     const QP p = J.qp[q];
     if (!(p.flags & 1)) return;
-    const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
     int base = J.areaOff[q];
     // enum_candidates visits in strided lane order; wrap each 64-candidate batch of a cell
     // range with a ballot so the output keeps the traversal order
@@ -594,7 +593,7 @@ __global__ void __launch_bounds__(256) k_area_fill(Job J) {
                 }
             }
             const uint64_t m = __ballot(keep);
-            if (keep) J.areaOut[base + __popcll(m & below)] = idx;
+            if (keep) J.areaOut[base + orbdev::lanes_below(m)] = idx;
             base += __popcll(m);
         }
     }
