@@ -156,6 +156,13 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
 }
 // Sum over the 64 lanes, wave-uniform.
 __device__ __forceinline__ int wave_total(int v) { return __builtin_amdgcn_readlane(wave_incl_scan(v), 63); }
+// m's bit for the calling lane ? if_set : if_clear, with the ballot mask itself as the condition
+// (v_cndmask on the SGPR pair: the compiler would otherwise compare the ballot's operand again)
+__device__ __forceinline__ int select_by_mask(uint64_t m, int if_clear, int if_set) {
+    int r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(if_clear), "v"(if_set), "s"(m));
+    return r;
+}
 // Set bits of a ballot mask below the calling lane: the lane's slot in a ballot-compacted append
 // (v_mbcnt_lo / v_mbcnt_hi on the mask's SGPR halves; popcount(m & lanes-below mask) took two
 // v_and and two v_bcnt on a per-lane VGPR mask)

@@ -921,11 +921,23 @@ __device__ __forceinline__ int fast_strength_packed(const uint8_t* p, int TP) {
 #else
     // a byte b read into a VGPR is the f16 denormal b * 2^-24: (v - c, c - v) is one v_pk_add_f16
     // of the two loaded bytes with both lanes on the low halves and one side negated per lane
-    // (exact: differences of denormals are exact; f16 denormals are not flushed)
+    // (exact: differences of denormals are exact; f16 denormals are not flushed).  The circle's
+    // bytes are read from one base per row (rows y-3 .. y+3, from column x-3) with the column as
+    // the ds_read immediate: seven address adds instead of one per circle point
+    constexpr int kDy[16] = {3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1, 0, 1, 2, 3};
+    constexpr int kDx[16] = {0, 1, 2, 3, 3, 3, 2, 1, 0, -1, -2, -3, -3, -3, -2, -1};
+    // (the base column x-3 made opaque: the compiler otherwise re-derives the bases from p and
+    // adds the negative column offsets separately, DS offsets being unsigned)
+    typedef const __attribute__((address_space(3))) uint8_t* lds_u8p;
+    uint32_t a0 = (uint32_t)(uintptr_t)(lds_u8p)p - 3u;
+    asm volatile("" : "+v"(a0));
+    lds_u8p rowp[7];
+#pragma unroll
+    for (int r = 0; r < 7; ++r) rowp[r] = (lds_u8p)(uintptr_t)(a0 + (uint32_t)((r - 3) * TP));
     f16x2_t d[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        const uint32_t c = p[off[k]];
+        const uint32_t c = rowp[kDy[k] + 3][kDx[k] + 3];
         uint32_t r;
         asm("v_pk_add_f16 %0, %1, %2 op_sel_hi:[0,0] neg_lo:[0,1] neg_hi:[1,0]" : "=v"(r) : "v"(v), "v"(c));
         d[k] = __builtin_bit_cast(f16x2_t, r);
@@ -1817,7 +1829,8 @@ __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, G
             for (int j = 0; j < 4; ++j) {  // expand the 64 entries into one pixel per slot
                 const bool v = (e >> j) & 1u;
                 const uint64_t m = __ballot(v);
-                px[v ? np + lanes_below(m) : FT_CQ] = (uint16_t)(code + j);
+                // every lane computes its slot, and the ballot itself selects it (one compare per bit)
+                px[select_by_mask(m, FT_CQ, np + lanes_below(m))] = (uint16_t)(code + j);
                 np += __popcll(m);
             }
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
