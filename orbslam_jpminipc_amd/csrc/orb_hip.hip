@@ -672,7 +672,111 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
     const int nq = slv[myL].nq, w = slv[myL].w, colOff = slv[myL].colOff;
     uint8_t* D = pyr + slv[myL].base + (long long)b * slv[myL].fstride;
     const int ql = (wave - ws) * 64 + lane, qs = 64 * nWaves;
-    lds_barrier();
+    // a level >= 1 column quad: its four columns' source offsets, weights and flags
+    struct QuadCols {
+        int sx[4];
+        uint32_t ap[4], live;  // ap = a0 | a1 << 16 (v_dot2 operand)
+        uint32_t simd;
+        bool allSimd;
+        uint32_t hmask;
+    };
+    auto decode_quad = [&](const uint4 cw) {
+        // column words: sx | a1 << 12 | (a0 - 2047 + a1) << 24 | simd << 26 | live << 27
+        QuadCols Q;
+        const uint32_t cc[4] = {cw.x, cw.y, cw.z, cw.w};
+        Q.live = 0;
+        Q.simd = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            Q.sx[j] = (int)(cc[j] & 0xFFFu);
+            const uint32_t a1 = (cc[j] >> 12) & 0xFFFu;
+            Q.ap[j] = (2047u + ((cc[j] >> 24) & 3u) - a1) | (a1 << 16);
+            if (cc[j] & (1u << 26)) Q.simd |= 1u << j;
+            if (cc[j] & (1u << 27)) Q.live |= 0xFFu << (8 * j);
+        }
+        Q.allSimd = Q.simd == 0xFu;
+        Q.hmask = Q.allSimd ? 0xFFFFFFF0u : 0xFFFFFFFFu;  // (H >> 4) << 4 on all-SSE2 quads
+        return Q;
+    };
+    auto build_quad = [&](const int q, const QuadCols& Q, const uint4* E, const int cnt) {
+        const int* sx = Q.sx;
+        const uint32_t* ap = Q.ap;
+        const uint32_t live = Q.live, simd = Q.simd, hmask = Q.hmask;
+        const bool allSimd = Q.allSimd;
+        // HResizeLinear of the source row at LDS address `ra`: H = S[sx] a0 + S[sx+1] a1
+        // (a1 == 0 where OpenCV reads S[sx] only: the byte after it is multiplied by 0; it
+        // lies in the ring row's slack or the next LDS row, never outside the allocation).
+        // On all-SSE2 quads h keeps (H >> 4) << 4 = H & ~15 for the v_mul_hi_u32_u24 below.
+        auto hrow = [&](uint32_t ra, uint32_t* hh) {
+            const uint8_t* R = s_ring + ra;
+            uint32_t lo8[4], hi8[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                lo8[j] = R[sx[j]];
+                hi8[j] = R[sx[j] + 1];
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t H = __builtin_amdgcn_udot2(__builtin_bit_cast(ps_u16x2, lo8[j] | (hi8[j] << 16)),
+                                                          __builtin_bit_cast(ps_u16x2, ap[j]), 0u, false);
+                hh[j] = H & hmask;
+            }
+        };
+        const int cx = 4 * q - EDGE;
+        const bool roi = cx >= 0 && cx < w;
+        uint32_t sA = 0xFFFFFFFFu, sB = 0xFFFFFFFFu;
+        uint32_t hA[4] = {0u, 0u, 0u, 0u}, hB[4] = {0u, 0u, 0u, 0u};
+        for (int k = 0; k < cnt; ++k) {
+            const uint4 e0 = E[2 * k], e1 = E[2 * k + 1];
+            const uint32_t s0 = e0.x, s1 = e0.y;
+            if (s0 != sA) {
+                if (s0 == sB) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) hA[j] = hB[j];
+                } else {
+                    hrow(s0, hA);
+                }
+                sA = s0;
+            }
+            if (s1 != sB) {
+                if (s1 == sA) {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) hB[j] = hA[j];
+                } else {
+                    hrow(s1, hB);
+                }
+                sB = s1;
+            }
+            uint32_t word = 0;
+            if (allSimd) {
+                // VResizeLinearVec_32s8u: ((H >> 4) * b) >> 16 per term = the high 32 bits of
+                // (H & ~15) * (b << 12) (both < 2^24), + 2 >> 2
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    word |= ((mulhi24(hA[j], e0.z) + mulhi24(hB[j], e0.w) + 2u) >> 2) << (8 * j);
+            } else {
+                const uint32_t b0 = e0.z >> 12, b1 = e0.w >> 12;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t r = ((simd >> j) & 1u)
+                                           ? ((__umul24(hA[j] >> 4, b0) >> 16) + (__umul24(hB[j] >> 4, b1) >> 16) + 2u) >> 2
+                                           : (__umul24(hA[j], b0) + __umul24(hB[j], b1) + (1u << 21)) >> 22;
+                    word |= r << (8 * j);
+                }
+            }
+            word &= live;
+            *(uint32_t*)(D + e1.y + 4 * q) = word;
+            if (e1.z != 0xFFFFFFFFu) *(uint32_t*)(D + e1.z + 4 * q) = word;
+            if (e1.w != 0xFFFFFFFFu) *(uint32_t*)(D + e1.w + 4 * q) = word;
+            if (e1.x != 0xFFFFFFFFu && roi) *(uint32_t*)(s_ring + e1.x + cx) = word;
+        }
+    };
+    // a level whose quads fit one pass of its waves (every level of 640-px frames): each lane's
+    // quad decoded once for the whole kernel instead of once per round
+    const bool hoisted = myL > 0 && !idle && nq <= qs;
+    lds_barrier();  // the column words are in LDS
+    QuadCols col0{};
+    if (hoisted) col0 = decode_quad(((const uint4*)(s_ring + colOff))[min(ql, nq - 1)]);
 #if PS_TIMING
     unsigned long long acc[5] = {0, 0, 0, 0, 0};
 #endif
@@ -709,11 +813,16 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
                         v = make_uint4(__builtin_amdgcn_perm(hi.w, hi.z, 0x03040506u), __builtin_amdgcn_perm(hi.z, hi.y, 0x03040506u),
                                        __builtin_amdgcn_perm(hi.y, hi.x, 0x03040506u), __builtin_amdgcn_perm(hi.x, lo.w, 0x03040506u));
                     } else {  // a border unit: single-bounce reflect-101 (w >= 17); all 16
-                              // reads unconditional (clamped), so they issue back to back
+                              // reads unconditional (clamped), so they issue back to back.  (The
+                              // compiler hoists the 16 indices out of the row loop for every unit;
+                              // keeping them in this branch measured slower: the border lanes share
+                              // the level-0 wave, which then ran them for every row, 0.394 vs
+                              // 0.380 ms c3)
+                        const int pxo = px;
                         uint32_t by[16];
 #pragma unroll
                         for (int j = 0; j < 16; ++j) {
-                            const int X = min(px + j - EDGE, w + EDGE - 1);
+                            const int X = min(pxo + j - EDGE, w + EDGE - 1);
                             by[j] = R[X < 0 ? -X : (X >= w ? 2 * w - 2 - X : X)];
                         }
                         uint32_t w4[4];
@@ -721,7 +830,7 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
                         for (int q4 = 0; q4 < 4; ++q4) {
                             uint32_t word = 0;
 #pragma unroll
-                            for (int j = 0; j < 4; ++j) word |= (px + 4 * q4 + j < w + 2 * EDGE ? by[4 * q4 + j] : 0u) << (8 * j);
+                            for (int j = 0; j < 4; ++j) word |= (pxo + 4 * q4 + j < w + 2 * EDGE ? by[4 * q4 + j] : 0u) << (8 * j);
                             w4[q4] = word;
                         }
                         v = make_uint4(w4[0], w4[1], w4[2], w4[3]);
@@ -733,90 +842,11 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
             }
         } else if (cnt > 0) {
             // level myL from the ring of level myL-1: per column unit, the round's rows in order
-            const uint4* C = (const uint4*)(s_ring + colOff);
-            for (int q = ql; q < nq; q += qs) {
-                // column words: sx | a1 << 12 | (a0 - 2047 + a1) << 24 | simd << 26 | live << 27
-                const uint4 cw = C[q];
-                const uint32_t cc[4] = {cw.x, cw.y, cw.z, cw.w};
-                int sx[4];
-                uint32_t ap[4], live = 0, simd = 0;  // ap = a0 | a1 << 16 (v_dot2 operand)
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    sx[j] = (int)(cc[j] & 0xFFFu);
-                    const uint32_t a1 = (cc[j] >> 12) & 0xFFFu;
-                    ap[j] = (2047u + ((cc[j] >> 24) & 3u) - a1) | (a1 << 16);
-                    if (cc[j] & (1u << 26)) simd |= 1u << j;
-                    if (cc[j] & (1u << 27)) live |= 0xFFu << (8 * j);
-                }
-                const bool allSimd = simd == 0xFu;
-                const uint32_t hmask = allSimd ? 0xFFFFFFF0u : 0xFFFFFFFFu;  // (H >> 4) << 4 on all-SSE2 quads
-                // HResizeLinear of the source row at LDS address `ra`: H = S[sx] a0 + S[sx+1] a1
-                // (a1 == 0 where OpenCV reads S[sx] only: the byte after it is multiplied by 0; it
-                // lies in the ring row's slack or the next LDS row, never outside the allocation).
-                // On all-SSE2 quads h keeps (H >> 4) << 4 = H & ~15 for the v_mul_hi_u32_u24 below.
-                auto hrow = [&](uint32_t ra, uint32_t* hh) {
-                    const uint8_t* R = s_ring + ra;
-                    uint32_t lo8[4], hi8[4];
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        lo8[j] = R[sx[j]];
-                        hi8[j] = R[sx[j] + 1];
-                    }
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const uint32_t H = __builtin_amdgcn_udot2(__builtin_bit_cast(ps_u16x2, lo8[j] | (hi8[j] << 16)),
-                                                                  __builtin_bit_cast(ps_u16x2, ap[j]), 0u, false);
-                        hh[j] = H & hmask;
-                    }
-                };
-                const int cx = 4 * q - EDGE;
-                const bool roi = cx >= 0 && cx < w;
-                uint32_t sA = 0xFFFFFFFFu, sB = 0xFFFFFFFFu;
-                uint32_t hA[4] = {0u, 0u, 0u, 0u}, hB[4] = {0u, 0u, 0u, 0u};
-                for (int k = 0; k < cnt; ++k) {
-                    const uint4 e0 = E[2 * k], e1 = E[2 * k + 1];
-                    const uint32_t s0 = e0.x, s1 = e0.y;
-                    if (s0 != sA) {
-                        if (s0 == sB) {
-#pragma unroll
-                            for (int j = 0; j < 4; ++j) hA[j] = hB[j];
-                        } else {
-                            hrow(s0, hA);
-                        }
-                        sA = s0;
-                    }
-                    if (s1 != sB) {
-                        if (s1 == sA) {
-#pragma unroll
-                            for (int j = 0; j < 4; ++j) hB[j] = hA[j];
-                        } else {
-                            hrow(s1, hB);
-                        }
-                        sB = s1;
-                    }
-                    uint32_t word = 0;
-                    if (allSimd) {
-                        // VResizeLinearVec_32s8u: ((H >> 4) * b) >> 16 per term = the high 32 bits of
-                        // (H & ~15) * (b << 12) (both < 2^24), + 2 >> 2
-#pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            word |= ((mulhi24(hA[j], e0.z) + mulhi24(hB[j], e0.w) + 2u) >> 2) << (8 * j);
-                    } else {
-                        const uint32_t b0 = e0.z >> 12, b1 = e0.w >> 12;
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            const uint32_t r = ((simd >> j) & 1u)
-                                                   ? ((__umul24(hA[j] >> 4, b0) >> 16) + (__umul24(hB[j] >> 4, b1) >> 16) + 2u) >> 2
-                                                   : (__umul24(hA[j], b0) + __umul24(hB[j], b1) + (1u << 21)) >> 22;
-                            word |= r << (8 * j);
-                        }
-                    }
-                    word &= live;
-                    *(uint32_t*)(D + e1.y + 4 * q) = word;
-                    if (e1.z != 0xFFFFFFFFu) *(uint32_t*)(D + e1.z + 4 * q) = word;
-                    if (e1.w != 0xFFFFFFFFu) *(uint32_t*)(D + e1.w + 4 * q) = word;
-                    if (e1.x != 0xFFFFFFFFu && roi) *(uint32_t*)(s_ring + e1.x + cx) = word;
-                }
+            if (hoisted) {
+                if (ql < nq) build_quad(ql, col0, E, cnt);
+            } else {
+                const uint4* C = (const uint4*)(s_ring + colOff);
+                for (int q = ql; q < nq; q += qs) build_quad(q, decode_quad(C[q]), E, cnt);
             }
         }
         PS_T(t2);
