@@ -2465,7 +2465,7 @@ struct MatchGeom {
 #ifndef KM_THREADS
 #define KM_THREADS 512  // one workgroup (8 waves) per pair: at most a few pairs share a CU
 #endif
-#define KM_LPQ (KM_THREADS / 256)  // phase-1 lanes per query (2 or 4)
+#define KM_WIDE_PAIRS 256  // fewer pairs: 16-wave workgroups (phase 1: NT / 256 lanes per query)
 #define MATCH_BIG_NMAX 8192
 #ifndef KM_TIMING  // 1: per-phase s_memrealtime sums of k_match_init's pairs (experiment builds only)
 #define KM_TIMING 0
@@ -2511,7 +2511,7 @@ __host__ __device__ inline size_t match_big_slot_bytes(int cap, int nmax) {
 }
 
 // Returns true (block-uniform) when the pair exceeded nmax and was left at -2 (-1 for BIG).
-template <bool BIG>
+template <bool BIG, int NT>
 __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, uint8_t* __restrict__ smem,
                                            uint8_t* __restrict__ gs) {
     constexpr int KB = BIG ? 13 : 11;  // slot bits of a (distance, slot) key
@@ -2573,14 +2573,14 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
     // ---- phase 0: keys in parallel, then ordered compaction ----
     // s_key[i2] = traversal key of F2 keypoint i2 or ~0 (not octave 0 / outside the grid);
     // s_m12[i1] = 1 if F1 keypoint i1 is a query (octave 0), as scratch.
-    for (int i = tid; i < n2; i += KM_THREADS) {
+    for (int i = tid; i < n2; i += NT) {
         const orb_keypoint_t kp = K2[i];
         const int px = (int)roundf((kp.x - mg.minX) * mg.invW);
         const int py = (int)roundf((kp.y - mg.minY) * mg.invH);
         const bool ok = kp.octave == 0 && !(px < 0 || px >= 64 || py < 0 || py >= 48);
         s_key[i] = ok ? (((uint32_t)(px * 48 + py) << 16) | (uint32_t)i) : 0xFFFFFFFFu;
     }
-    for (int i = tid; i < n1; i += KM_THREADS) s_m12[i] = K1[i].octave == 0;  // level1 > 0 -> continue (ORBmatcher.cc:615)
+    for (int i = tid; i < n1; i += NT) s_m12[i] = K1[i].octave == 0;  // level1 > 0 -> continue (ORBmatcher.cc:615)
     if constexpr (BIG) __threadfence_block();
     __syncthreads();
     if (wave == 0) {  // in-place, in-order compaction (one wave: reads precede writes)
@@ -2613,7 +2613,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
     }
     KM_T(1);
     // rank F2 candidates by traversal key -> slot
-    for (int t = tid; t < n2c; t += KM_THREADS) {
+    for (int t = tid; t < n2c; t += NT) {
         const uint32_t k = s_key[t];
         int rank = 0;
         for (int u = 0; u < n2c; ++u) rank += s_key[u] < k;
@@ -2627,7 +2627,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
 #pragma unroll
         for (int w = 0; w < 8; ++w) s_d2[rank * 8 + w] = D2[(long long)i2 * 8 + w];
     }
-    for (int q = tid; q < n1c; q += KM_THREADS) {
+    for (int q = tid; q < n1c; q += NT) {
         const int i1 = s_q2i[q];
         const orb_keypoint_t kp = K1[i1];
         s_qx[q] = prev ? prev[((long long)p * cap + i1) * 2] : kp.x;
@@ -2635,7 +2635,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
     }
     if constexpr (BIG) __threadfence_block();
     __syncthreads();
-    for (int i = tid; i < n1; i += KM_THREADS) {
+    for (int i = tid; i < n1; i += NT) {
         s_m12[i] = -1;
         s_bslot[i] = -1;
     }
@@ -2654,8 +2654,8 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
     KM_T(2);
     // ---- phase 1: per-query top-8 (dist, order), two lanes per query (candidates j of one
     // parity each), their sorted lists merged on DPP ----
-    for (int q0 = 0; q0 < n1c; q0 += KM_THREADS / KM_LPQ) {
-        const int q = q0 + tid / KM_LPQ, sub = tid & (KM_LPQ - 1);
+    for (int q0 = 0; q0 < n1c; q0 += NT / (NT / 256)) {
+        const int q = q0 + tid / (NT / 256), sub = tid & ((NT / 256) - 1);
         const bool act = q < n1c;
         float qx = 0.f, qy = 0.f;
         int minCX = 1, maxCX = 0, minCY = 1, maxCY = 0;
@@ -2680,7 +2680,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
         int cnt = 0;
         // the window's grid columns only (an empty column range gives j0 >= j1)
         const int j0 = s_col[min(minCX, 64)], j1 = s_col[max(maxCX + 1, 0)];
-        for (int j = j0 + sub; j < j1; j += KM_LPQ) {
+        for (int j = j0 + sub; j < j1; j += (NT / 256)) {
             // every read of the candidate issued at once (one LDS round trip per candidate, not
             // three dependent ones behind the window tests; prefetching the next candidate's
             // reads one iteration ahead measured slower: 15.8 vs 13.6 us per pair alone)
@@ -2720,7 +2720,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
                     }
         };
         merge_round(std::integral_constant<int, 0xB1>{});
-        if constexpr (KM_LPQ == 4) merge_round(std::integral_constant<int, 0x4E>{});
+        if constexpr ((NT / 256) == 4) merge_round(std::integral_constant<int, 0x4E>{});
         if (act && sub == 0) {
 #pragma unroll
             for (int k = 0; k < MATCH_TOPK; ++k) s_list[q * MATCH_TOPK + k] = m8[k];
@@ -2847,7 +2847,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
         if (tid < 32) s_hist[tid] = 0;
         __syncthreads();
         // rotation bin of every accepted i1, the stolen ones included (ORBmatcher.cc:664-676)
-        for (int i = tid; i < n1; i += KM_THREADS) {
+        for (int i = tid; i < n1; i += NT) {
             const int sl = s_bslot[i];
             if (sl < 0) continue;
             float rot = K1[i].angle - s_a2[sl];
@@ -2891,14 +2891,14 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
         }
         __syncthreads();
         const int i1x = s_ind[0], i2x = s_ind[1], i3x = s_ind[2];
-        for (int i = tid; i < n1; i += KM_THREADS) {
+        for (int i = tid; i < n1; i += NT) {
             const int bn = s_bslot[i];
             if (bn >= 0 && bn != i1x && bn != i2x && bn != i3x) s_m12[i] = -1;
         }
         __syncthreads();
     }
     int nm = 0;
-    for (int i = tid; i < n1; i += KM_THREADS) {
+    for (int i = tid; i < n1; i += NT) {
         const int m = s_m12[i];
         A.m12out[(long long)p * cap + i] = m;
         if (m >= 0) {
@@ -2915,7 +2915,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
     if (tid == 0) {
         int t = 0;
 #pragma unroll
-        for (int w = 0; w < KM_THREADS / 64; ++w) t += s_hist[w];
+        for (int w = 0; w < NT / 64; ++w) t += s_hist[w];
         A.nmOut[p] = t;
     }
 #if KM_TIMING
@@ -2939,12 +2939,16 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
 // keypoints), its staged arrays in the pair's own slot of the global scratch `big` (null when
 // cap <= A.nmax: nothing can overflow).  The dynamic LDS covers both bodies' needs, so no
 // second launch and nothing per call beyond this kernel.
-__global__ void __launch_bounds__(KM_THREADS) k_match_init(MatchArgs A, uint8_t* __restrict__ big, int nmaxBig) {
+// NT threads: KM_THREADS (8 waves) when pairs share CUs; 16 waves when each pair has a CU to
+// itself (fewer pairs than KM_WIDE_PAIRS, e.g. one SearchForInitialization call): phase 1 then
+// scores each query with four lanes instead of two.
+template <int NT>
+__global__ void __launch_bounds__(NT) k_match_init(MatchArgs A, uint8_t* __restrict__ big, int nmaxBig) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int p = blockIdx.x;
-    if (match_pair<false>(A, p, A.nmax, smem, nullptr) && big) {
+    if (match_pair<false, NT>(A, p, A.nmax, smem, nullptr) && big) {
         __syncthreads();  // the static LDS (counts, bins) is reused
-        match_pair<true>(A, p, nmaxBig, smem, big + (size_t)p * match_big_slot_bytes(A.cap, nmaxBig));
+        match_pair<true, NT>(A, p, nmaxBig, smem, big + (size_t)p * match_big_slot_bytes(A.cap, nmaxBig));
     }
 }
 
@@ -4284,7 +4288,10 @@ int orb_search_for_initialization_batch_device(const orb_keypoint_t* d_kps, cons
         return set_err(ORB_ENOTSUP, "per-frame keypoint capacity too large for LDS");
     static std::once_flag attrOnce;
     std::call_once(attrOnce, [] {
-        (void)hipFuncSetAttribute((const void*)k_match_init, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_match_init<KM_THREADS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  159 * 1024);
+        (void)hipFuncSetAttribute((const void*)k_match_init<2 * KM_THREADS>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
         (void)hipGetLastError();  // an unsupported attribute value must not surface as the launch's error
     });
     MatchGeom mg{bounds.min_x, bounds.max_x, bounds.min_y, bounds.max_y,
@@ -4299,7 +4306,10 @@ int orb_search_for_initialization_batch_device(const orb_keypoint_t* d_kps, cons
         lk.lock();     // held until the launch that uses it is enqueued
         if (int r = match_big_scratch_locked(st, match_big_slot_bytes(cap, nmaxBig) * (size_t)P, &big)) return r;
     }
-    hipLaunchKernelGGL(k_match_init, dim3(P), dim3(KM_THREADS), lds, st, A, (uint8_t*)big, nmaxBig);
+    if (P < KM_WIDE_PAIRS)
+        hipLaunchKernelGGL(k_match_init<2 * KM_THREADS>, dim3(P), dim3(2 * KM_THREADS), lds, st, A, (uint8_t*)big, nmaxBig);
+    else
+        hipLaunchKernelGGL(k_match_init<KM_THREADS>, dim3(P), dim3(KM_THREADS), lds, st, A, (uint8_t*)big, nmaxBig);
     HIP_TRY(hipGetLastError());
     return ORB_OK;
 }
@@ -4318,16 +4328,18 @@ int orb_search_for_initialization(const orb_keypoint_t* kps1, const uint8_t* des
     if (n1 > MATCH_BIG_NMAX || n2 > MATCH_BIG_NMAX) return set_err(ORB_ENOTSUP, "more than 8192 keypoints in a frame");
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));
-    // the calling thread's context: grow-only device arena + pinned staging, its own stream
-    // (no per-call allocation, no device-wide synchronisation)
+    // the calling thread's context: grow-only pinned staging, its own stream (no per-call
+    // allocation, no device-wide synchronisation).  The kernel reads its inputs from the pinned
+    // staging and writes vnMatches12 / vbPrevMatched / nmatches back into it: no H2D or D2H
+    // command (one SearchForInitialization call 64 -> 57 us at 640x480 / 1000 kp,
+    // scripts/sfi_breakdown.cpp)
     OrbHostCtx* C = orb_internal_thread_ctx(dev);
     if (!C) return set_err(ORB_EINVAL, "device ordinal out of range");
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     const size_t oK = 0, oD = oK + al((size_t)2 * cap * sizeof(orb_keypoint_t)), oC = oD + al((size_t)2 * cap * 32),
                  oP = oC + al(6 * sizeof(int)), oM = oP + al((size_t)cap * 8), total = oM + al((size_t)cap * 4 + 4);
-    if (int r = C->reserve(total, total)) return r;
+    if (int r = C->reserve(0, total)) return r;
     uint8_t* hs = C->pinned;
-    uint8_t* ds = C->buf;
     std::memcpy(hs + oK, kps1, (size_t)n1 * sizeof(orb_keypoint_t));
     if (n2) std::memcpy(hs + oK + (size_t)cap * sizeof(orb_keypoint_t), kps2, (size_t)n2 * sizeof(orb_keypoint_t));
     std::memcpy(hs + oD, desc1, (size_t)n1 * 32);
@@ -4336,17 +4348,13 @@ int orb_search_for_initialization(const orb_keypoint_t* kps1, const uint8_t* des
     std::memcpy(hs + oC, hostc, sizeof(hostc));
     std::memcpy(hs + oP, prev_xy, (size_t)n1 * 8);
     hipStream_t s = C->stream;
-    HIP_TRY(hipMemcpyAsync(ds, hs, oM, hipMemcpyHostToDevice, s));
-    int* dc = (int*)(ds + oC);
-    int* dm = (int*)(ds + oM);
-    int st = orb_search_for_initialization_batch_device((const orb_keypoint_t*)(ds + oK), ds + oD, dc, cap, 1, dc + 2,
-                                                        dc + 3, bounds, nnratio, check_ori, window, (float*)(ds + oP),
+    int* dc = (int*)(hs + oC);
+    int* dm = (int*)(hs + oM);
+    int st = orb_search_for_initialization_batch_device((const orb_keypoint_t*)(hs + oK), hs + oD, dc, cap, 1, dc + 2,
+                                                        dc + 3, bounds, nnratio, check_ori, window, (float*)(hs + oP),
                                                         dm, dm + cap, s);
-    hipError_t e = hipSuccess;  // vbPrevMatched and vnMatches12 + nmatches are adjacent: one D2H copy
-    if (!st) e = hipMemcpyAsync(hs + oP, ds + oP, oM + (size_t)cap * 4 + 4 - oP, hipMemcpyDeviceToHost, s);
-    hipError_t es = hipStreamSynchronize(s);  // always drained: the staging is reused by the next call
+    const hipError_t e = hipStreamSynchronize(s);  // always drained: the staging is reused by the next call
     if (st) return st;
-    if (e == hipSuccess) e = es;
     if (e != hipSuccess) return set_err(ORB_EDEVICE, std::string("match: ") + hipGetErrorString(e));
     int nm = 0;
     std::memcpy(&nm, hs + oM + (size_t)cap * 4, 4);
