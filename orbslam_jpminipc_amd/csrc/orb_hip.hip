@@ -1114,7 +1114,7 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
                 for (int j = 0; j < 4; ++j) {
                     const bool c = (mask >> j) & 1u;
                     const uint64_t bm = __ballot(c);
-                    q[c ? np + lanes_below(bm) : RR_Q] = (uint32_t)(px0 + j);  // RR_Q: trash slot
+                    q[select_by_mask(bm, RR_Q, np + lanes_below(bm))] = (uint32_t)(px0 + j);  // RR_Q: trash slot
                     np += __popcll(bm);
                 }
             }
@@ -1176,7 +1176,7 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
             for (int j = 0; j < 4; ++j) {
                 const bool v = ((w4 >> (8 * j)) & 0xFFu) != 0u;
                 const uint64_t m = __ballot(v);
-                q[v ? cn + lanes_below(m) : RR_Q] = ((uint32_t)yy << 16) | (uint32_t)(4 * wd + j);
+                q[select_by_mask(m, RR_Q, cn + lanes_below(m))] = ((uint32_t)yy << 16) | (uint32_t)(4 * wd + j);
                 cn += __popcll(m);
             }
             if (cn > RR_Q - 256) {
@@ -1942,7 +1942,7 @@ __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, G
             for (int j = 0; j < KF_DPL; ++j) {
                 const bool v = m[j] != 0u;
                 const uint64_t bm = __ballot(v);
-                pq[v ? qn + lanes_below(bm) : FT_Q] = (uint16_t)(((uint32_t)(fq + j) << 4) | m[j]);
+                pq[select_by_mask(bm, FT_Q, qn + lanes_below(bm))] = (uint16_t)(((uint32_t)(fq + j) << 4) | m[j]);
                 qn += (int)__popcll(bm);
             }
         }
@@ -2002,7 +2002,7 @@ __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, G
             }
             // survivors overwrite the front of the list (k0 + 64 > sn: no unread entry is hit)
             const uint64_t m = __ballot(keep);
-            pq[keep ? sn + lanes_below(m) : FT_Q] = e;
+            pq[select_by_mask(m, FT_Q, sn + lanes_below(m))] = e;
             sn += __popcll(m);
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -2041,7 +2041,7 @@ __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, G
             for (int j = 0; j < 4; ++j) {
                 const bool v = ((w4 >> (8 * j)) & 0xFFu) != 0u;
                 const uint64_t m = __ballot(v);
-                pq[v ? cn + lanes_below(m) : FT_Q] = (uint16_t)((r << 9) | (4 * d + j));
+                pq[select_by_mask(m, FT_Q, cn + lanes_below(m))] = (uint16_t)((r << 9) | (4 * d + j));
                 cn += __popcll(m);
             }
             if (cn > FT_Q - 256) {
