@@ -14,20 +14,23 @@
 //
 // One 1024-thread workgroup per pair (16 waves: 4 waves per pair left 2 waves per SIMD at 511
 // pairs, 0.388 ms per c3 step):
-//   1. each thread binary-searches KF node positions in the other vector's node list (LDS);
+//   0. (where both frames fit, cap <= ~1800) their descriptors, feature lists, node offsets and
+//      B's node ids are copied into LDS by all threads, so the node loop below touches LDS only;
+//   1. each thread binary-searches KF node positions in the other vector's node list;
 //   2. wave w takes the common nodes w, w+16, ...: per query (wave-uniform) every lane scores the
-//      node's candidates it holds (<= 64 candidates: one per lane, descriptor in registers for
-//      the whole node; more: strided, reloaded), key = (distance << 16) | candidate position, and
-//      two wave-min reductions give the reference's bestDist1 / bestIdx (first minimum in
-//      candidate order) and bestDist2; an accepted query marks its target in LDS and writes the
-//      output; the histogram counts by LDS atomics;
-//   3. ComputeThreeMaxima (ORBmatcher.cc:1748-1789) and the removal pass (bins recomputed from
-//      the keypoint angles of the kept outputs).
+//      node's candidates it holds (<= 64 candidates: one per lane, descriptor and matched flag
+//      in registers for the whole node; more: strided, reloaded, flags in LDS), key =
+//      (distance << 16) | candidate position, and two wave-min reductions give the reference's
+//      bestDist1 / bestIdx (first minimum in candidate order) and bestDist2; an accepted query
+//      marks its target and writes the output;
+//   3. the rotation histogram from the outputs, ComputeThreeMaxima (ORBmatcher.cc:1748-1789) and
+//      the removal pass (bins recomputed from the keypoint angles of the kept outputs).
 // Latency-bound by design (sequential queries per node); SURVEY §8d-style bytes per pair:
 // 32 B per feature of both frames + 4 B per output slot.
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <mutex>
 #include <string>
 
 #include "../../include/orb_abi.h"
@@ -73,6 +76,18 @@ struct BowBatch {
     float nnratio;
 };
 
+// LDS bytes of the staged variant: both frames' descriptors, feature-vector feature lists and
+// node offsets, the usable flags of A and B's node ids, on top of the per-pair state (5 cap)
+__host__ __device__ inline size_t bow_stage_bytes(int cap) {
+    return ((5 * (size_t)cap + 15) & ~(size_t)15) + 64 * (size_t)cap + 8 * (size_t)cap + 8 * ((size_t)cap + 1) +
+           (((size_t)cap + 3) & ~(size_t)3) + 4 * (size_t)cap;
+}
+
+// STAGE: both frames' descriptors, feature lists and node offsets are copied into LDS first (all
+// threads, coalesced), so a node's queries run on LDS only; without it every node pays ~5
+// dependent global round trips (offsets, candidate indices -> descriptors, query indices ->
+// flags / descriptors) on its wave.
+template <bool STAGE>
 __global__ void __launch_bounds__(BOW_T) k_bow_pairs(BowBatch J) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ int s_hist[HISTO];
@@ -85,34 +100,63 @@ __global__ void __launch_bounds__(BOW_T) k_bow_pairs(BowBatch J) {
     const int nodesA = min(J.fvN[fa], nA), nodesB = min(J.fvN[fb], nB);
     const uint32_t* NA = J.fvNodes + (size_t)fa * cap;
     const uint32_t* NB = J.fvNodes + (size_t)fb * cap;
-    const int32_t* OA = J.fvOff + (size_t)fa * (cap + 1);
-    const int32_t* OB = J.fvOff + (size_t)fb * (cap + 1);
-    const int32_t* FA = J.fvFeat + (size_t)fa * cap;
-    const int32_t* FB = J.fvFeat + (size_t)fb * cap;
+    const int32_t* gOA = J.fvOff + (size_t)fa * (cap + 1);
+    const int32_t* gOB = J.fvOff + (size_t)fb * (cap + 1);
+    const int32_t* gFA = J.fvFeat + (size_t)fa * cap;
+    const int32_t* gFB = J.fvFeat + (size_t)fb * cap;
     const orb_keypoint_t* KA = J.kps + (size_t)fa * cap;
     const orb_keypoint_t* KB = J.kps + (size_t)fb * cap;
-    const uint4* DA = (const uint4*)(J.desc + (size_t)fa * cap * 32);
-    const uint4* DB = (const uint4*)(J.desc + (size_t)fb * cap * 32);
-    const uint8_t* UA = J.usable ? J.usable + (size_t)fa * cap : nullptr;
+    const uint4* gDA = (const uint4*)(J.desc + (size_t)fa * cap * 32);
+    const uint4* gDB = (const uint4*)(J.desc + (size_t)fb * cap * 32);
+    const uint8_t* gUA = J.usable ? J.usable + (size_t)fa * cap : nullptr;
     const uint8_t* UB = J.usable ? J.usable + (size_t)fb * cap : nullptr;
     int32_t* out = J.match + (size_t)p * cap;
     const int nOut = J.kfkf ? nA : nB;  // vpMatches12 over KF1 / vpMapPointMatches over F
     int* s_mb = (int*)smem;                   // [cap] KF node position -> other node position or -1
     uint8_t* s_taken = smem + 4 * (size_t)cap;  // [cap] other-side features matched (or unusable)
+    // the staged copies (STAGE), after the per-pair state
+    uint4* sDA = (uint4*)(smem + ((5 * (size_t)cap + 15) & ~(size_t)15));
+    uint4* sDB = sDA + 2 * (size_t)cap;
+    int* sFA = (int*)(sDB + 2 * (size_t)cap);
+    int* sFB = sFA + cap;
+    int* sOA = sFB + cap;
+    int* sOB = sOA + cap + 1;
+    uint8_t* sUA = (uint8_t*)(sOB + cap + 1);
+    uint32_t* sNB = (uint32_t*)(sUA + ((cap + 3) & ~3));
+    const uint4* DA = STAGE ? sDA : gDA;
+    const uint4* DB = STAGE ? sDB : gDB;
+    const int32_t* FA = STAGE ? sFA : gFA;
+    const int32_t* FB = STAGE ? sFB : gFB;
+    const int32_t* OA = STAGE ? sOA : gOA;
+    const int32_t* OB = STAGE ? sOB : gOB;
+    const uint8_t* UA = STAGE ? (gUA ? sUA : nullptr) : gUA;
 
     for (int i = tid; i < cap; i += BOW_T) out[i] = -1;
     for (int i = tid; i < nB; i += BOW_T) s_taken[i] = (J.kfkf && UB) ? (uint8_t)(UB[i] == 0) : (uint8_t)0;
+    if constexpr (STAGE) {
+        for (int i = tid; i < 2 * nA; i += BOW_T) sDA[i] = gDA[i];
+        for (int i = tid; i < 2 * nB; i += BOW_T) sDB[i] = gDB[i];
+        for (int i = tid; i <= nodesA; i += BOW_T) sOA[i] = gOA[i];
+        for (int i = tid; i <= nodesB; i += BOW_T) sOB[i] = gOB[i];
+        for (int i = tid; i < nA; i += BOW_T) sFA[i] = gFA[i];  // (a vector's features: at most its frame's)
+        for (int i = tid; i < nB; i += BOW_T) sFB[i] = gFB[i];
+        if (gUA)
+            for (int i = tid; i < nA; i += BOW_T) sUA[i] = gUA[i];
+        for (int i = tid; i < nodesB; i += BOW_T) sNB[i] = NB[i];
+        __syncthreads();  // the lower_bound below searches B's node ids in LDS
+    }
+    const uint32_t* NBs = STAGE ? sNB : NB;
     for (int a = tid; a < nodesA; a += BOW_T) {  // the merge walk's common nodes (lower_bound)
         const uint32_t id = NA[a];
         int lo = 0, hi = nodesB;
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
-            if (NB[mid] < id)
+            if (NBs[mid] < id)
                 lo = mid + 1;
             else
                 hi = mid;
         }
-        s_mb[a] = (lo < nodesB && NB[lo] == id) ? lo : -1;
+        s_mb[a] = (lo < nodesB && NBs[lo] == id) ? lo : -1;
     }
     if (tid < HISTO) s_hist[tid] = 0;
     if (tid == 0) s_acc = 0, s_rem = 0;
@@ -128,13 +172,15 @@ __global__ void __launch_bounds__(BOW_T) k_bow_pairs(BowBatch J) {
         // <= 64 candidates: one per lane, descriptor held for the whole node
         int myIdx = 0;
         uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
+        bool myTaken = true;  // the lane's candidate matched (or unusable): a node's own state, in a register
         if (small && lane < nc) {
             myIdx = min((unsigned)FB[c0 + lane], (unsigned)(nB - 1));  // (clamped: never outside the frame)
             m0 = DB[2 * (size_t)myIdx];
             m1 = DB[2 * (size_t)myIdx + 1];
+            myTaken = s_taken[myIdx] != 0;
         }
         // the node's queries 64 at a time: lane j loads query j's index, flag and descriptor (one
-        // global round trip per 64 queries), each query then takes them by v_readlane
+        // round trip per 64 queries), each query then takes them by v_readlane
         int qIdx = 0, qOk = 0;
         uint4 qd0 = make_uint4(0, 0, 0, 0), qd1 = qd0;
         for (int q = q0; q < q1; ++q) {
@@ -159,7 +205,7 @@ __global__ void __launch_bounds__(BOW_T) k_bow_pairs(BowBatch J) {
             d1.z = __builtin_amdgcn_readlane(qd1.z, j), d1.w = __builtin_amdgcn_readlane(qd1.w, j);
             uint32_t k1 = NONE, k2 = NONE;  // this lane's two smallest keys
             if (small) {
-                if (lane < nc && !s_taken[myIdx]) k1 = ((uint32_t)ham(d0, d1, m0, m1) << 16) | (uint32_t)lane;
+                if (!myTaken) k1 = ((uint32_t)ham(d0, d1, m0, m1) << 16) | (uint32_t)lane;
             } else {
                 for (int j = lane; j < nc; j += 64) {
                     const int idx2 = FB[c0 + j];
@@ -183,22 +229,34 @@ __global__ void __launch_bounds__(BOW_T) k_bow_pairs(BowBatch J) {
             if (!(thOk && (float)dist1 < J.nnratio * (float)dist2)) continue;
             const int jb = (int)(b1 & 0xFFFFu);
             const int idx2 = small ? __builtin_amdgcn_readlane(myIdx, jb) : FB[c0 + jb];
-            if (lane == 0) {
+            if (small) {
+                if (lane == jb) myTaken = true;  // (a candidate is in exactly one node)
+            } else if (lane == 0) {
                 s_taken[idx2] = 1;
+            }
+            if (lane == 0) {
                 if (J.kfkf)
                     out[idx1] = idx2;  // vpMatches12[idx1] = vpMapPoints2[bestIdx2]
                 else
                     out[idx2] = idx1;  // vpMapPointMatches[bestIdxF] = pMP (the KF feature)
-                if (J.checkOri) atomicAdd(&s_hist[rot_bin(KA[idx1].angle, KB[idx2].angle)], 1);
                 ++acc;
             }
-            // lane 0's LDS write lands before any lane's next read (same wave, in order)
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            // (large nodes) lane 0's LDS write lands before any lane's next read (same wave, in order)
+            if (!small) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
     }
     if (lane == 0 && acc) atomicAdd(&s_acc, acc);
-    __syncthreads();  // (also orders the output writes before the removal pass reads them)
+    __syncthreads();  // (also orders the output writes before the histogram / removal passes read them)
     if (J.checkOri) {
+        // rotHist (ORBmatcher.cc:230-236 / 799-805) from the accepted pairs: an accepted pair is
+        // never revisited, so the outputs are exactly the pairs pushed into the histogram (built
+        // here in parallel, not by one lane per accept behind two dependent keypoint loads)
+        for (int i = tid; i < nOut; i += BOW_T) {
+            const int v = out[i];
+            if (v >= 0)
+                atomicAdd(&s_hist[J.kfkf ? rot_bin(KA[i].angle, KB[v].angle) : rot_bin(KA[v].angle, KB[i].angle)], 1);
+        }
+        __syncthreads();
         if (tid == 0) {  // ComputeThreeMaxima (ORBmatcher.cc:1748-1789)
             int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
             for (int i = 0; i < HISTO; ++i) {
@@ -254,8 +312,17 @@ extern "C" int orb_search_by_bow_batch_device(int kf_kf, const orb_keypoint_t* d
     if (((uintptr_t)d_desc & 15) != 0) return orb_internal_set_error(ORB_EINVAL, "descriptors must be 16-B aligned");
     BowBatch J{d_kps, d_desc, d_counts, d_fv_nodes, d_fv_offsets, d_fv_features, d_fv_n, d_pair_a, d_pair_b,
                d_usable, d_match, d_nmatches, cap, kf_kf, check_ori ? 1 : 0, nnratio};
-    const size_t lds = 5 * (size_t)cap;
-    hipLaunchKernelGGL(k_bow_pairs, dim3(P), dim3(BOW_T), lds, (hipStream_t)stream, J);
+    // both frames staged in LDS where they fit (cap <= ~1870 keypoints per frame)
+    const size_t ldsStage = bow_stage_bytes(cap);
+    static std::once_flag attrOnce;
+    std::call_once(attrOnce, [] {
+        (void)hipFuncSetAttribute((const void*)k_bow_pairs<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 159 * 1024);
+        (void)hipGetLastError();
+    });
+    if (ldsStage <= 159 * 1024)
+        hipLaunchKernelGGL(k_bow_pairs<true>, dim3(P), dim3(BOW_T), ldsStage, (hipStream_t)stream, J);
+    else
+        hipLaunchKernelGGL(k_bow_pairs<false>, dim3(P), dim3(BOW_T), 5 * (size_t)cap, (hipStream_t)stream, J);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return orb_internal_set_error(ORB_EDEVICE, std::string("k_bow_pairs: ") + hipGetErrorString(e));
     return ORB_OK;
