@@ -905,6 +905,45 @@ __device__ __forceinline__ uint32_t compass4(uint32_t c, uint32_t q0, uint32_t q
     return compass_mask(compass_half(even_bytes(c), even_bytes(q0), even_bytes(q4), even_bytes(q8), even_bytes(q12), tt),
                         compass_half(odd_bytes(c), odd_bytes(q0), odd_bytes(q4), odd_bytes(q8), odd_bytes(q12), tt));
 }
+#ifndef KR_COMPASS8
+#define KR_COMPASS8 1
+#endif
+// cv::FAST's full pre-test (all eight even circle points): a 9-arc holds a point of every
+// antipodal pair {k, k+8}, so bright <=> min over the four pairs of their max > v + t and dark
+// <=> max over the pairs of their min < v - t are necessary.  Stronger than compass_half (two
+// pairs), for the FAST(7) re-runs whose low threshold lets most noisy pixels through the compass.
+__device__ __forceinline__ uint32_t compass8_half(uint32_t v, uint32_t q0, uint32_t q8, uint32_t q4, uint32_t q12,
+                                                  uint32_t q2, uint32_t q10, uint32_t q6, uint32_t q14, uint32_t tt) {
+    const u16x2 a0 = __builtin_bit_cast(u16x2, q0), a8 = __builtin_bit_cast(u16x2, q8);
+    const u16x2 a4 = __builtin_bit_cast(u16x2, q4), a12 = __builtin_bit_cast(u16x2, q12);
+    const u16x2 a2 = __builtin_bit_cast(u16x2, q2), a10 = __builtin_bit_cast(u16x2, q10);
+    const u16x2 a6 = __builtin_bit_cast(u16x2, q6), a14 = __builtin_bit_cast(u16x2, q14);
+    const i16x2 M = __builtin_bit_cast(
+        i16x2, __builtin_elementwise_min(
+                   __builtin_elementwise_min(__builtin_elementwise_max(a0, a8), __builtin_elementwise_max(a4, a12)),
+                   __builtin_elementwise_min(__builtin_elementwise_max(a2, a10), __builtin_elementwise_max(a6, a14))));
+    const i16x2 m = __builtin_bit_cast(
+        i16x2, __builtin_elementwise_max(
+                   __builtin_elementwise_max(__builtin_elementwise_min(a0, a8), __builtin_elementwise_min(a4, a12)),
+                   __builtin_elementwise_max(__builtin_elementwise_min(a2, a10), __builtin_elementwise_min(a6, a14))));
+    const i16x2 vv = __builtin_bit_cast(i16x2, v);
+    const i16x2 X = __builtin_elementwise_max((i16x2)(M - vv), (i16x2)(vv - m));
+    return __builtin_bit_cast(uint32_t, (i16x2)(__builtin_bit_cast(i16x2, tt) - X));
+}
+// the eight-point pre-test of one dword from its centre row (dwords -1, 0, +1: lf, cc, rg), the rows
+// 3 below / above (dn, up) and the rows 2 below / above (dwords -1, 0, +1: d2*, u2*)
+__device__ __forceinline__ uint32_t compass8(uint32_t lf, uint32_t cc, uint32_t rg, uint32_t dn, uint32_t up,
+                                             uint32_t d2l, uint32_t d2c, uint32_t d2r, uint32_t u2l, uint32_t u2c,
+                                             uint32_t u2r, uint32_t tt) {
+    const uint32_t q4 = __builtin_amdgcn_alignbyte(rg, cc, 3), q12 = __builtin_amdgcn_alignbyte(cc, lf, 1);
+    // circle points 2 = (+2, +2), 14 = (+2, -2) on the row 2 below; 6 = (-2, +2), 10 = (-2, -2) 2 above
+    const uint32_t q2 = __builtin_amdgcn_alignbyte(d2r, d2c, 2), q14 = __builtin_amdgcn_alignbyte(d2c, d2l, 2);
+    const uint32_t q6 = __builtin_amdgcn_alignbyte(u2r, u2c, 2), q10 = __builtin_amdgcn_alignbyte(u2c, u2l, 2);
+    return compass_mask(compass8_half(even_bytes(cc), even_bytes(dn), even_bytes(up), even_bytes(q4), even_bytes(q12),
+                                      even_bytes(q2), even_bytes(q10), even_bytes(q6), even_bytes(q14), tt),
+                        compass8_half(odd_bytes(cc), odd_bytes(dn), odd_bytes(up), odd_bytes(q4), odd_bytes(q12),
+                                      odd_bytes(q2), odd_bytes(q10), odd_bytes(q6), odd_bytes(q14), tt));
+}
 
 // ---- FAST strength --------------------------------------------------------------------------
 // S(p) = 1 + cornerScore<16>(p) of cv::FAST: the largest t for which p is a corner is S - 1,
@@ -1106,8 +1145,14 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
                     const int xx0 = 4 * wd - 3 - o;  // detection column of byte 0
                     const int lo = max(0, -xx0), hi = min(4, dw - xx0);
                     const uint32_t cols = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+#if KR_COMPASS8
+                    const uint32_t* d2 = row + 2 * iw;
+                    const uint32_t* u2 = row - 2 * iw;
+                    mask = compass8(lf, cc, rg, dn, up, d2[-1], d2[0], d2[1], u2[-1], u2[0], u2[1], tt) & cols;
+#else
                     mask = compass4(cc, dn, __builtin_amdgcn_alignbyte(rg, cc, 3), up,
                                     __builtin_amdgcn_alignbyte(cc, lf, 1), tt) & cols;
+#endif
                     px0 = yy * dw + xx0;
                 }
 #pragma unroll
