@@ -622,9 +622,14 @@ __device__ unsigned long long g_pstime[32];
 __global__ void __launch_bounds__(PS_THREADS) __attribute__((amdgpu_waves_per_eu(PS_WAVES)))
 k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uint8_t* __restrict__ pyr,
              const uint32_t* __restrict__ colWords, const uint4* __restrict__ rowEntries,
-             const StreamLevel* __restrict__ slv, const uint32_t* __restrict__ rounds, StreamGeom sg) {
+             const StreamLevel* __restrict__ slv, const uint32_t* __restrict__ rounds, StreamGeom sg,
+             int* __restrict__ cellCount, int nCells) {
     extern __shared__ __attribute__((aligned(16))) uint8_t s_ring[];
     const int b = blockIdx.x, tid = threadIdx.x;
+    // the frame's per-cell FAST counters for k_fast (when this launch is followed by the rest of
+    // the extraction: one memset launch fewer)
+    if (cellCount)
+        for (int i = tid; i < nCells; i += PS_THREADS) cellCount[(long long)b * nCells + i] = 0;
     const int rw = sg.L + 2;  // words per round record
     for (int i = tid; i < sg.colWords; i += PS_THREADS) ((uint32_t*)(s_ring + sg.colOff))[i] = colWords[i];
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -3848,6 +3853,7 @@ struct orb_extractor {
             int r = profile_collect();
             if (r) return r;
         }
+        bool countsZeroed = false;  // k_pyr_stream zeroed k_fast's cell counters
         if ((phases & 1u) && cn == 1 && streamOk && (B >= KR_STREAM_BATCH || pyrStreamAlways) && !pyrLegacy) {
             // the whole pyramid in one streaming pass per frame (stage 0; stage 1 is empty)
             stage_begin(0, st);
@@ -3856,7 +3862,8 @@ struct orb_extractor {
             sg.align = (al & 15u) == 0 ? 16 : (al & 3u) == 0 ? 4 : 1;
             hipLaunchKernelGGL(k_pyr_stream, dim3(B), dim3(PS_THREADS), streamLds, st, d_imgs, stride, fpitch, d_pyr,
                                (const uint32_t*)d_scol, (const uint4*)d_srows, (const StreamLevel*)d_slv,
-                               (const uint32_t*)d_srounds, sg);
+                               (const uint32_t*)d_srounds, sg, (phases & 2u) ? d_cellCount : (int*)nullptr, g.nCells);
+            countsZeroed = (phases & 2u) != 0;
             stage_end(0, st);
             pyrBatch = B;
         } else if (phases & 1u) {
@@ -3899,7 +3906,7 @@ struct orb_extractor {
             return ORB_OK;
         }
         stage_begin(2, st);
-        HIP_TRY(hipMemsetAsync(d_cellCount, 0, (size_t)g.nCells * B * 4, st));
+        if (!countsZeroed) HIP_TRY(hipMemsetAsync(d_cellCount, 0, (size_t)g.nCells * B * 4, st));
         hipLaunchKernelGGL(k_fast, dim3(nTiles, B), dim3(256), 0, st, d_pyr, g, d_tiles, d_cand, d_cellCount);
         stage_end(2, st);
         stage_begin(3, st);
