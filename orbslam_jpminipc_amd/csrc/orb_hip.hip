@@ -1443,12 +1443,42 @@ __device__ __forceinline__ int cell_of(const int* off, int n, int i) {
 #define KS_WAVES 2  // waves per SIMD the register allocation targets
 #endif
 
+// The last of a frame's L k_select workgroups to finish writes the frame's per-level (first output
+// slot, count) pairs and total (what k_lvl_prefix did in a launch of its own): each workgroup's
+// thread 0 publishes its level count with an agent-scope atomic store (past its XCD's L2: the
+// frame's workgroups run on different XCDs), waits for it, then counts itself in selDone[b];
+// the one that brings it to L reads the L counts with agent-scope atomic loads and resets
+// selDone[b] for the next launch.  (A __threadfence() release here writes back the L2 of every
+// workgroup: +60 us per c3 step.)
+__device__ __forceinline__ void select_frame_done(int b, int L, int l, int keep, int* __restrict__ lvlCount,
+                                                  int* __restrict__ selDone, int2* __restrict__ lvlInfo,
+                                                  int* __restrict__ counts) {
+    __hip_atomic_store(&lvlCount[(long long)b * L + l], keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (__hip_atomic_fetch_add(&selDone[b], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != L - 1) return;
+    int c[ORB_MAX_LEVELS];
+#pragma unroll
+    for (int l = 0; l < ORB_MAX_LEVELS; ++l)
+        c[l] = __hip_atomic_load(&lvlCount[(long long)b * L + min(l, L - 1)], __ATOMIC_RELAXED,  // (in bounds:
+                                 __HIP_MEMORY_SCOPE_AGENT);                                      // all issued at once)
+    int before = 0;
+#pragma unroll
+    for (int l = 0; l < ORB_MAX_LEVELS; ++l)
+        if (l < L) {
+            lvlInfo[(long long)b * ORB_MAX_LEVELS + l] = make_int2(before, c[l]);
+            before += c[l];
+        }
+    counts[b] = before;
+    __hip_atomic_store(&selDone[b], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <bool HARRIS, bool RERUN>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAVES))) k_select(const uint8_t* __restrict__ pyr, uint32_t* __restrict__ cand,
                                                 uint32_t* __restrict__ cand2, int* __restrict__ cellCount, Geom g,
                                                 const CellGeom* __restrict__ cells, uint32_t* __restrict__ lvlOut,
                                                 int* __restrict__ lvlCount, uint64_t* __restrict__ candH,
-                                                float* __restrict__ lvlResp, float harrisScale4) {
+                                                float* __restrict__ lvlResp, float harrisScale4, int* __restrict__ selDone,
+                                                int2* __restrict__ lvlInfo, int* __restrict__ counts) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     __shared__ int s_cnt[ORB_MAX_CELLS_PER_LEVEL];
     __shared__ int s_ret[ORB_MAX_CELLS_PER_LEVEL];
@@ -1680,7 +1710,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
             lvlOut[ob + k] = (uint32_t)v;
             lvlResp[ob + k] = __uint_as_float((uint32_t)(v >> 32));
         }
-        if (tid == 0) lvlCount[(long long)b * g.L + l] = keep;
+        if (tid == 0) {
+            select_frame_done(b, g.L, l, keep, lvlCount, selDone, lvlInfo, counts);
+        }
         return;
     }
     // (4) retainBest per cell, then the level list in cell order, then retainBest to the quota
@@ -1730,7 +1762,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
     KS_T(5);
     uint32_t* out = lvlOut + (long long)b * g.kpCap + lg.kpBase;
     for (int k = tid; k < keep; k += 256) out[k] = list[k];
-    if (tid == 0) lvlCount[(long long)b * g.L + l] = keep;
+    if (tid == 0) {
+        select_frame_done(b, g.L, l, keep, lvlCount, selDone, lvlInfo, counts);
+    }
 #if KS_TIMING
     // phases: 0 counts + re-runs, 1 bookkeeping, 2 load + raster sort, 3 per-cell retainBest,
     // 4 level list + level retainBest, 5 output; [6] = survivors M, [7] = workgroups
@@ -2194,24 +2228,6 @@ __device__ __forceinline__ uint32_t blur_round(uint32_t T, bool tail) {
                     // two slots per wave, lanes 0-31 / 32-63, 2 or 4 waves per workgroup: 0.531 / 0.567 vs
                     // 0.428 ms c3, 1.018 / 1.093 vs 0.818 c4 -- half the waves per CU, longer chains)
 #endif
-// Per frame and level: (keypoints of the frame's earlier levels, keypoints of this level) =
-// where the level's keypoints start in the frame's output (level-major, ORBextractor.cc:749-778)
-// and how many there are; and the frame's total (the count the reference returns).  One thread
-// per frame, after k_select: k_orient_desc then reads one pair per wave instead of summing the
-// per-level counts itself.
-__global__ void __launch_bounds__(256) k_lvl_prefix(const int* __restrict__ lvlCount, int L, int B,
-                                                    int2* __restrict__ lvlInfo, int* __restrict__ counts) {
-    const int b = blockIdx.x * 256 + threadIdx.x;
-    if (b >= B) return;
-    int before = 0;
-    for (int l = 0; l < L; ++l) {
-        const int c = lvlCount[(long long)b * L + l];
-        lvlInfo[(long long)b * ORB_MAX_LEVELS + l] = make_int2(before, c);
-        before += c;
-    }
-    counts[b] = before;
-}
-
 __global__ void __launch_bounds__(64 * OD_WAVES) k_orient_desc(const uint8_t* __restrict__ pyr, Geom g,
                                                      const uint32_t* __restrict__ lvlOut,
                                                      const uint8_t* __restrict__ slotLvl,
@@ -2236,7 +2252,7 @@ __global__ void __launch_bounds__(64 * OD_WAVES) k_orient_desc(const uint8_t* __
     const uint32_t fslot = (uint32_t)b * (uint32_t)g.kpCap;
     const uint32_t e = (uint32_t)__builtin_amdgcn_readfirstlane((int)lvlOut[fslot + (uint32_t)kc]);
     // the slot's level: one byte of the host-built slot -> level table (a scalar load beside the
-    // record's), then the frame's (first output slot, count) of that level from k_lvl_prefix
+    // record's), then the frame's (first output slot, count) of that level (select_frame_done)
     const uint32_t lw = *(const uint32_t*)(slotLvl + (kc & ~3));
     const int l = (int)((lw >> (8 * (kc & 3))) & 0xFFu);
     const int2 linfo = lvlInfo[(uint32_t)b * ORB_MAX_LEVELS + (uint32_t)l];
@@ -3069,7 +3085,8 @@ struct orb_extractor {
     uint32_t* d_cand2 = nullptr;  // k_select scratch when a level's survivors exceed its LDS
     uint32_t* d_lvl = nullptr;
     int* d_lvlCount = nullptr;
-    int2* d_lvlInfo = nullptr;     // [frame][ORB_MAX_LEVELS] (first output slot, count): k_lvl_prefix
+    int2* d_lvlInfo = nullptr;     // [frame][ORB_MAX_LEVELS] (first output slot, count): k_select's last WG
+    int* d_selDone = nullptr;      // [frame] k_select workgroups done (self-resetting, zero between launches)
     uint8_t* d_slotLvl = nullptr;  // keypoint slot -> level (kpCap bytes, padded to a dword)
     uint64_t* d_candH = nullptr;  // HARRIS_SCORE: (response, record) scratch when a level exceeds LDS
     float* d_lvlResp = nullptr;   // HARRIS_SCORE: response of every kept keypoint
@@ -3124,6 +3141,7 @@ struct orb_extractor {
         hipFree(d_lvl);
         hipFree(d_lvlCount);
         hipFree(d_lvlInfo);
+        hipFree(d_selDone);
         hipFree(d_slotLvl);
         hipFree(d_candH);
         hipFree(d_lvlResp);
@@ -3151,6 +3169,7 @@ struct orb_extractor {
         d_lvl = nullptr;
         d_lvlCount = nullptr;
         d_lvlInfo = nullptr;
+        d_selDone = nullptr;
         d_slotLvl = nullptr;
         d_candH = nullptr;
         d_lvlResp = nullptr;
@@ -3474,6 +3493,8 @@ struct orb_extractor {
         HIP_TRY(hipMalloc(&d_lvl, (size_t)std::max(kpCap, 1) * maxBatch * 4));
         HIP_TRY(hipMalloc(&d_lvlCount, (size_t)nlevels * maxBatch * 4));
         HIP_TRY(hipMalloc(&d_lvlInfo, (size_t)ORB_MAX_LEVELS * maxBatch * sizeof(int2)));
+        HIP_TRY(hipMalloc(&d_selDone, (size_t)maxBatch * sizeof(int)));
+        HIP_TRY(hipMemset(d_selDone, 0, (size_t)maxBatch * sizeof(int)));
         {
             std::vector<uint8_t> sl(((size_t)std::max(kpCap, 1) + 3) & ~(size_t)3, 0);
             for (int l = 0; l < nlevels; ++l)
@@ -3924,21 +3945,24 @@ struct orb_extractor {
         if (scoreType == ORB_HARRIS_SCORE) {
             if (sep)
                 hipLaunchKernelGGL((k_select<true, false>), sg, dim3(256), listLds, st, d_pyr, d_cand, d_cand2,
-                                   d_cellCount, g, d_cells, d_lvl, d_lvlCount, d_candH, d_lvlResp, harrisScale4);
+                                   d_cellCount, g, d_cells, d_lvl, d_lvlCount, d_candH, d_lvlResp, harrisScale4, d_selDone,
+                                   d_lvlInfo, counts);
             else
                 hipLaunchKernelGGL((k_select<true, true>), sg, dim3(256), selectLds, st, d_pyr, d_cand, d_cand2,
-                                   d_cellCount, g, d_cells, d_lvl, d_lvlCount, d_candH, d_lvlResp, harrisScale4);
+                                   d_cellCount, g, d_cells, d_lvl, d_lvlCount, d_candH, d_lvlResp, harrisScale4, d_selDone,
+                                   d_lvlInfo, counts);
         } else {
             if (sep)
                 hipLaunchKernelGGL((k_select<false, false>), sg, dim3(256), listLds, st, d_pyr, d_cand, d_cand2,
-                                   d_cellCount, g, d_cells, d_lvl, d_lvlCount, (uint64_t*)nullptr, (float*)nullptr, 0.f);
+                                   d_cellCount, g, d_cells, d_lvl, d_lvlCount, (uint64_t*)nullptr, (float*)nullptr, 0.f,
+                                   d_selDone, d_lvlInfo, counts);
             else
                 hipLaunchKernelGGL((k_select<false, true>), sg, dim3(256), selectLds, st, d_pyr, d_cand, d_cand2,
-                                   d_cellCount, g, d_cells, d_lvl, d_lvlCount, (uint64_t*)nullptr, (float*)nullptr, 0.f);
+                                   d_cellCount, g, d_cells, d_lvl, d_lvlCount, (uint64_t*)nullptr, (float*)nullptr, 0.f,
+                                   d_selDone, d_lvlInfo, counts);
         }
-        // the frames' per-level output offsets and totals (part of the selection stage)
-        hipLaunchKernelGGL(k_lvl_prefix, dim3((B + 255) / 256), dim3(256), 0, st, d_lvlCount, nlevels, B, d_lvlInfo,
-                           counts);
+        // (the frames' per-level output offsets and totals: written by each frame's last k_select
+        // workgroup, select_frame_done)
         stage_end(3, st);
         stage_begin(4, st);
         dim3 gd((std::max(kpCap, 1) + OD_WAVES - 1) / OD_WAVES, B);

@@ -4,7 +4,10 @@ constant tables (row-pass B fragments, IC disc masks, rBRIEF pattern) read throu
 pointers passed as a kernel argument (hipGetSymbolAddress; global loads at 32-bit byte
 offsets) instead of through the __constant__ symbols.  `scripts/r04_diag.sh NAME` on the result
 reproduces the nondeterministic descriptor bits recorded in DESIGN.md §6.
-Usage: od_tables_variant.py NAME  ->  build/variants/NAME.so"""
+Usage: od_tables_variant.py NAME  ->  build/variants/NAME.so
+Its text anchors are those of orb_hip.hip at commit 17303d2 (before round 5's IC-table change
+replaced the disc masks); build that revision's sources to rerun it
+(`git archive 17303d2 orbslam_jpminipc_amd/csrc include`)."""
 import subprocess, sys
 reps = [
  ("__constant__ uint4 c_rowB[4 * 64];  // 279 patch dwords per alignment, zero-padded to 5 x 64\n",
@@ -19,8 +22,8 @@ reps = [
   "    for (int j = 0; j < 5; ++j) icm[j] = OD_LD(uint32_t, icmask, 4u * (320u * (uint32_t)((x + 1 - xa) & 3) + (uint32_t)lane + 64u * j));"),
  ("        const float4 f = ((const float4*)c_patternf)[lane * 4 + q];",
   "        typedef float f32x4v __attribute__((ext_vector_type(4)));\n        const f32x4v f = OD_LD(f32x4v, patf, 16u * (4u * (uint32_t)lane + q));"),
- ("    int2* d_lvlInfo = nullptr;     // [frame][ORB_MAX_LEVELS] (first output slot, count): k_lvl_prefix\n",
-  "    int2* d_lvlInfo = nullptr;     // [frame][ORB_MAX_LEVELS] (first output slot, count): k_lvl_prefix\n    ODTables odTables{};\n"),
+ ("    int2* d_lvlInfo = nullptr;     // [frame][ORB_MAX_LEVELS] (first output slot, count): k_select's last WG\n",
+  "    int2* d_lvlInfo = nullptr;     // [frame][ORB_MAX_LEVELS] (first output slot, count): k_select's last WG\n    ODTables odTables{};\n"),
  ("desc, (const float*)d_lvlResp);", "desc, (const float*)d_lvlResp, odTables);"),
  ("    int st = upload_pattern(device);\n",
   "    int st = upload_pattern(device);\n    ODTables odt{};\n    HIP_TRY(hipGetSymbolAddress((void**)&odt.rowB, HIP_SYMBOL(c_rowB)));\n    HIP_TRY(hipGetSymbolAddress((void**)&odt.icmask, HIP_SYMBOL(c_icmask)));\n    HIP_TRY(hipGetSymbolAddress((void**)&odt.patf, HIP_SYMBOL(c_patternf)));\n"),
