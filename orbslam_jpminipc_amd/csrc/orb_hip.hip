@@ -2568,6 +2568,14 @@ struct MatchArgs {
     int P;
 };
 
+// ORBmatcher.cc:664-670: the rotation's histogram bin (HISTO_LENGTH 30, factor 1/30)
+__device__ __forceinline__ int rot_bin30(float rot) {
+    if (rot < 0.0f) rot += 360.0f;
+    int bin = (int)roundf(rot * (1.0f / 30));
+    if (bin == 30) bin = 0;
+    return bin;
+}
+
 // Byte size of one global scratch slot of the large-capacity body (nmax slots / queries).
 __host__ __device__ inline size_t match_big_slot_bytes(int cap, int nmax) {
     // d2 32 + x2,y2,a2,cell 16 per F2 slot; q2i,qx,qy,lcnt 16 per query; top-8 lists
@@ -2601,7 +2609,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
     // y = the F2 keypoint index — one LDS read gives the greedy pass all it needs of a slot
     uint32_t* s_d2;
     uint2* s_st;
-    float *s_x2, *s_y2, *s_qx, *s_qy, *s_a2;
+    float *s_x2, *s_y2, *s_qx, *s_qy, *s_a2, *s_a1 = nullptr;
     int *s_cell, *s_q2i, *s_lcnt, *s_m12;
     uint32_t* s_list;
     short* s_bslot;
@@ -2618,7 +2626,8 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
         s_list = (uint32_t*)(s_a2 + nmax);        // nmax x TOPK
         s_lcnt = (int*)(s_list + (size_t)nmax * MATCH_TOPK);
         s_m12 = s_lcnt + nmax;                    // vnMatches12 (cap)
-        s_bslot = (short*)(s_m12 + cap);          // F2 slot of each accepted i1, then its rotation bin (cap)
+        s_bslot = (short*)(s_m12 + cap);          // F2 slot of each accepted i1 (cap)
+        s_a1 = (float*)(s_bslot + ((cap + 1) & ~1));  // F1 query angles by keypoint index (cap)
     } else {
         s_st = (uint2*)smem;                      // LDS: greedy state
         s_m12 = (int*)(s_st + nmax);
@@ -2698,6 +2707,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
         const orb_keypoint_t kp = K1[i1];
         s_qx[q] = prev ? prev[((long long)p * cap + i1) * 2] : kp.x;
         s_qy[q] = prev ? prev[((long long)p * cap + i1) * 2 + 1] : kp.y;
+        if constexpr (!BIG) s_a1[i1] = kp.angle;  // (only queries are ever accepted)
     }
     if constexpr (BIG) __threadfence_block();
     __syncthreads();
@@ -2912,16 +2922,12 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
     if (A.checkOri) {
         if (tid < 32) s_hist[tid] = 0;
         __syncthreads();
-        // rotation bin of every accepted i1, the stolen ones included (ORBmatcher.cc:664-676)
+        // rotation bin of every accepted i1, the stolen ones included (ORBmatcher.cc:664-676); the
+        // angles from LDS (s_a1 / s_a2), the slot kept for the output pass
         for (int i = tid; i < n1; i += NT) {
             const int sl = s_bslot[i];
             if (sl < 0) continue;
-            float rot = K1[i].angle - s_a2[sl];
-            if (rot < 0.0f) rot += 360.0f;
-            int bin = (int)roundf(rot * (1.0f / 30));
-            if (bin == 30) bin = 0;
-            s_bslot[i] = (short)bin;
-            atomicAdd(&s_hist[bin], 1);
+            atomicAdd(&s_hist[rot_bin30((BIG ? K1[i].angle : s_a1[i]) - s_a2[sl])], 1);
         }
         __syncthreads();
         if (tid == 0) {  // ComputeThreeMaxima (ORBmatcher.cc:1748-1789)
@@ -2958,8 +2964,10 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
         __syncthreads();
         const int i1x = s_ind[0], i2x = s_ind[1], i3x = s_ind[2];
         for (int i = tid; i < n1; i += NT) {
-            const int bn = s_bslot[i];
-            if (bn >= 0 && bn != i1x && bn != i2x && bn != i3x) s_m12[i] = -1;
+            const int sl = s_bslot[i];
+            if (sl < 0) continue;
+            const int bn = rot_bin30((BIG ? K1[i].angle : s_a1[i]) - s_a2[sl]);
+            if (bn != i1x && bn != i2x && bn != i3x) s_m12[i] = -1;
         }
         __syncthreads();
     }
@@ -2969,9 +2977,10 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
         A.m12out[(long long)p * cap + i] = m;
         if (m >= 0) {
             nm++;
-            if (prev) {
-                prev[((long long)p * cap + i) * 2] = K2[m].x;
-                prev[((long long)p * cap + i) * 2 + 1] = K2[m].y;
+            if (prev) {  // vbPrevMatched[i1] = F2.mvKeysUn[i2].pt: the accepted slot's staged position
+                const int sl = s_bslot[i];
+                prev[((long long)p * cap + i) * 2] = s_x2[sl];
+                prev[((long long)p * cap + i) * 2 + 1] = s_y2[sl];
             }
         }
     }
@@ -4263,8 +4272,8 @@ int orb_descriptor_distance(const uint8_t* a, const uint8_t* b) {
 #endif
 static size_t match_lds_bytes(int cap, int nmax) {
     // F2 slots (desc 32 + state 8 + x,y,a,cell 16) + queries (q2i,qx,qy 12 + top-8 32 + cnt 4)
-    // + cap x (m12 4 + slot/bin 2)
-    return (size_t)nmax * (56 + 48) + (size_t)cap * 6 + 16;
+    // + cap x (m12 4 + slot 2 + query angle 4)
+    return (size_t)nmax * (56 + 48) + (size_t)cap * 10 + 32;
 }
 static size_t match_big_lds_bytes(int cap, int nmax) { return (size_t)nmax * 8 + (size_t)cap * 6 + 16; }
 
