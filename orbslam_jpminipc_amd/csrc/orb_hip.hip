@@ -770,9 +770,15 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
                 }
             }
             word &= live;
-            *(uint32_t*)(D + e1.y + 4 * q) = word;
-            if (e1.z != 0xFFFFFFFFu) *(uint32_t*)(D + e1.z + 4 * q) = word;
-            if (e1.w != 0xFFFFFFFFu) *(uint32_t*)(D + e1.w + 4 * q) = word;
+            // wave-uniform row base (SGPRs) + the lane's 32-bit offset: no 64-bit VALU address
+            // add per store and row (nothing in this kernel reads the pyramid back)
+            const uint32_t qo = 4u * (uint32_t)q;
+            auto store_row = [&](uint32_t off) {
+                asm volatile("global_store_dword %0, %1, %2" ::"v"(qo), "v"(word), "s"(D + off) : "memory");
+            };
+            store_row(e1.y);
+            if (e1.z != 0xFFFFFFFFu) store_row(e1.z);
+            if (e1.w != 0xFFFFFFFFu) store_row(e1.w);
             if (e1.x != 0xFFFFFFFFu && roi) *(uint32_t*)(s_ring + e1.x + cx) = word;
         }
     };
