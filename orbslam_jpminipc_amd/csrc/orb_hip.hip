@@ -729,29 +729,8 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
         };
         const int cx = 4 * q - EDGE;
         const bool roi = cx >= 0 && cx < w;
-        uint32_t sA = 0xFFFFFFFFu, sB = 0xFFFFFFFFu;
-        uint32_t hA[4] = {0u, 0u, 0u, 0u}, hB[4] = {0u, 0u, 0u, 0u};
-        for (int k = 0; k < cnt; ++k) {
-            const uint4 e0 = E[2 * k], e1 = E[2 * k + 1];
-            const uint32_t s0 = e0.x, s1 = e0.y;
-            if (s0 != sA) {
-                if (s0 == sB) {
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) hA[j] = hB[j];
-                } else {
-                    hrow(s0, hA);
-                }
-                sA = s0;
-            }
-            if (s1 != sB) {
-                if (s1 == sA) {
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) hB[j] = hA[j];
-                } else {
-                    hrow(s1, hB);
-                }
-                sB = s1;
-            }
+        // one output row from its two source rows' horizontal sums hA (row s0) and hB (row s1)
+        auto vrow = [&](const uint4 e0, const uint4 e1, const uint32_t* hA, const uint32_t* hB) {
             uint32_t word = 0;
             if (allSimd) {
                 // VResizeLinearVec_32s8u: ((H >> 4) * b) >> 16 per term = the high 32 bits of
@@ -780,6 +759,26 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
             if (e1.z != 0xFFFFFFFFu) store_row(e1.z);
             if (e1.w != 0xFFFFFFFFu) store_row(e1.w);
             if (e1.x != 0xFFFFFFFFu && roi) *(uint32_t*)(s_ring + e1.x + cx) = word;
+        };
+        // Rows in pairs with the source roles alternating: even rows read (hP, hQ), odd rows
+        // (hQ, hP).  A downscale step's next row starts at this row's second source row (held
+        // in the set the next row reads first), so only the other set is recomputed, and no
+        // row ever copies sums between register sets.  (tP / tQ: the rows they hold.)
+        uint32_t tP = 0xFFFFFFFFu, tQ = 0xFFFFFFFFu;
+        uint32_t hP[4] = {0u, 0u, 0u, 0u}, hQ[4] = {0u, 0u, 0u, 0u};
+        for (int k = 0; k < cnt; k += 2) {
+            {
+                const uint4 e0 = E[2 * k], e1 = E[2 * k + 1];
+                if (tP != e0.x) hrow(e0.x, hP), tP = e0.x;
+                if (tQ != e0.y) hrow(e0.y, hQ), tQ = e0.y;
+                vrow(e0, e1, hP, hQ);
+            }
+            if (k + 1 < cnt) {
+                const uint4 e0 = E[2 * k + 2], e1 = E[2 * k + 3];
+                if (tQ != e0.x) hrow(e0.x, hQ), tQ = e0.x;
+                if (tP != e0.y) hrow(e0.y, hP), tP = e0.y;
+                vrow(e0, e1, hQ, hP);
+            }
         }
     };
     // a level whose quads fit one pass of its waves (every level of 640-px frames): each lane's
