@@ -356,30 +356,8 @@ __global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, c
         }
     };
     uint8_t* D = pyr + lg.base + (long long)b * lg.fstride + x4;
-    int rA = -1, rB = -1;  // source rows held in hA / hB (wave-uniform)
-    uint32_t hA[4] = {0, 0, 0, 0}, hB[4] = {0, 0, 0, 0};
-    for (int py = pyA; py < pyB; ++py) {
-        const int sy = __builtin_amdgcn_readlane(rowSy, py - pyA);
-        const uint32_t bb = (uint32_t)__builtin_amdgcn_readlane(rowBeta, py - pyA);
-        const int s0 = min(max(sy, 0), ls.h - 1), s1 = min(max(sy + 1, 0), ls.h - 1);
-        if (s0 != rA) {
-            if (s0 == rB) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) hA[i] = hB[i];
-            } else {
-                hrow(s0, hA);
-            }
-            rA = s0;
-        }
-        if (s1 != rB) {
-            if (s1 == rA) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) hB[i] = hA[i];
-            } else {
-                hrow(s1, hB);
-            }
-            rB = s1;
-        }
+    // one output row from the horizontal sums hA (source row s0) and hB (s1)
+    auto vrow = [&](const int py, const uint32_t bb, const uint32_t* hA, const uint32_t* hB) {
         const uint32_t b0 = bb & 0xFFFFu, b1 = bb >> 16;
         uint32_t word;
         if (allSimd) {
@@ -402,6 +380,35 @@ __global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, c
             }
         }
         *(uint32_t*)(D + (long long)py * lg.pitch) = word & liveMask;
+    };
+    // rows in pairs with the source register sets in alternating roles (k_pyr_stream's
+    // build_quad): a downscale row's second source row is the next row's first, already in the
+    // set that row reads first, so no sums are copied between sets (tP / tQ: rows held)
+    int tP = -1, tQ = -1;
+    uint32_t hP[4] = {0, 0, 0, 0}, hQ[4] = {0, 0, 0, 0};
+    auto src_rows = [&](const int py, int& s0, int& s1, uint32_t& bb) {
+        const int sy = __builtin_amdgcn_readlane(rowSy, py - pyA);
+        bb = (uint32_t)__builtin_amdgcn_readlane(rowBeta, py - pyA);
+        s0 = min(max(sy, 0), ls.h - 1);
+        s1 = min(max(sy + 1, 0), ls.h - 1);
+    };
+    for (int py = pyA; py < pyB; py += 2) {
+        {
+            int s0, s1;
+            uint32_t bb;
+            src_rows(py, s0, s1, bb);
+            if (tP != s0) hrow(s0, hP), tP = s0;
+            if (tQ != s1) hrow(s1, hQ), tQ = s1;
+            vrow(py, bb, hP, hQ);
+        }
+        if (py + 1 < pyB) {
+            int s0, s1;
+            uint32_t bb;
+            src_rows(py + 1, s0, s1, bb);
+            if (tQ != s0) hrow(s0, hQ), tQ = s0;
+            if (tP != s1) hrow(s1, hP), tP = s1;
+            vrow(py + 1, bb, hQ, hP);
+        }
     }
 }
 
