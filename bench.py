@@ -70,7 +70,7 @@ SALU_PEAK = N_CU * CLOCK_HZ  # SALU instructions / s: one scalar unit per CU, on
 LDS_PEAK = N_CU * CLOCK_HZ   # LDS pipe cycles / s: one per CU per cycle
 # Measured VALU issue rate of the 4-cycle instruction kinds (v_perm, v_pk_*, v_alignbyte, v_bfe,
 # v_dot*, v_mul_*24, v_min/max_u32, DPP moves, 3-source VOP3) with 8 waves per SIMD, all CUs busy:
-# 0.58 wave64 instructions per ns per SIMD (scripts/valu_rate.hip, profiles/r05_valu_rate.json;
+# 0.58 wave64 instructions per ns per SIMD (scripts/gen_valu_rate.py, profiles/r05_valu_rate.json;
 # add / and / or / shift / f32 fma reach 1.08 alone, but a 1:1 mix with a 4-cycle kind runs 0.61)
 VALU_4C_PEAK = N_CU * 4 * 0.58e9
 METRIC = "frames/sec ORB extract+match, 640x480 8-level 1000 kp; HBM GB/s vs peak"

@@ -149,8 +149,10 @@ struct CellGeom {
 // ======================================================================================
 using namespace orbdev;
 
-__constant__ signed char c_pattern[1024];
-__constant__ float c_patternf[1024];  // the same pattern as floats: lane l's 8 points are 4 float4
+// bit_pattern_31_ (ORBextractor.cc:197-455) as floats, pair-major: c_patternf[2 (64 q + l) + {0, 1}]
+// = (x, y) of point 8 l + q, i.e. lane l's eight points are one float2 in each of eight 512-B
+// rows (k_orient_desc loads each row with one fully coalesced global_load_dwordx2, §6.1)
+__constant__ float c_patternf[1024];
 // IC_Angle (ORBextractor.cc:124-151 with umax, 495-510) over the 31 x 9 patch dwords n = 9 r + c
 // (five 64-lane steps, n < 320; n >= 279 carry zero coefficients): c_icoff[n] = the dword's byte
 // offset in k_orient_desc's window from the patch's first dword; per byte alignment sh of the
@@ -1460,14 +1462,18 @@ __device__ __forceinline__ int cell_of(const int* off, int n, int i) {
 // thread 0 publishes its level count with an agent-scope atomic store (past its XCD's L2: the
 // frame's workgroups run on different XCDs), waits for it, then counts itself in selDone[b];
 // the one that brings it to L reads the L counts with agent-scope atomic loads and resets
-// selDone[b] for the next launch.  (A __threadfence() release here writes back the L2 of every
-// workgroup: +60 us per c3 step.)
+// selDone[b] for the next launch.  Ordering: the only data handed over (lvlCount) is written and
+// read with agent-scope atomics, which bypass the XCD's L2, and the writer waits for its store to
+// complete (vmcnt(0)) before it counts itself; the last workgroup then takes an agent-scope
+// acquire (one L1 / L2 invalidate, on that workgroup only) before its loads.  (A __threadfence()
+// release on every workgroup writes back the L2 of each: +60 us per c3 step.)
 __device__ __forceinline__ void select_frame_done(int b, int L, int l, int keep, int* __restrict__ lvlCount,
                                                   int* __restrict__ selDone, int2* __restrict__ lvlInfo,
                                                   int* __restrict__ counts) {
     __hip_atomic_store(&lvlCount[(long long)b * L + l], keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (__hip_atomic_fetch_add(&selDone[b], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != L - 1) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     int c[ORB_MAX_LEVELS];
 #pragma unroll
     for (int l = 0; l < ORB_MAX_LEVELS; ++l)
@@ -1842,6 +1848,12 @@ struct FastTile {
 #ifndef KF_DPL
 #define KF_DPL 2  // adjacent dwords per lane and step of the compass loop (1, 2 or 4)
 #endif
+#ifndef KF_B64
+#define KF_B64 1  // compass groups on 8-B aligned dword pairs read with ds_read_b64 (KF_DPL 2 only)
+#endif
+#if KF_B64
+static_assert(KF_DPL == 2, "KF_B64 reads the groups' dword pairs");
+#endif
 __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, Geom g,
                                                       const FastTile* __restrict__ tiles,
                                                       uint32_t* __restrict__ cand, int* __restrict__ cellCount) {
@@ -1853,8 +1865,9 @@ __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, G
     __shared__ uint16_t s_px[4][FT_CQ + 2];  // a chunk's pixels, compacted in place to its corners
     __shared__ uint16_t s_cl[4][FT_CL + 2];  // the wave's interior corners (tile row << 9 | tile column)
     __shared__ int s_ovf;                    // a wave's corner list overflowed: scan the plane
-    __shared__ uint8_t s_cm[FT_TW_MAX / 4 + 2 + KF_DPL];  // per flattened dword column: its detection
-                                                           // pixels (0 past the ring)
+    __shared__ uint8_t s_cm[FT_TW_MAX / 4 + 3 + KF_DPL];  // per flattened dword column: its detection
+                                                           // pixels (0 past the ring; KF_B64: index
+                                                           // dc + 1, 0 at dc = -1)
     KF_T(0);
     // (plain block order: an XCD-aware order, vertically adjacent tiles on one XCD so their halo
     // rows hit in its L2, measured slower -- 0.646 vs 0.574 ms c3: the halo is not what binds)
@@ -1902,6 +1915,13 @@ __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, G
         const int nS = ((t.th + 2) * spw + 15) >> 4;
         for (int i = tid; i < nS; i += 256) ((uint4*)s_S)[i] = make_uint4(0u, 0u, 0u, 0u);
         if (tid == 0) s_ovf = 0;
+#if KF_B64
+        if (tid < fw + 3) {
+            const int dc = tid - 1, X = t.x0 + 4 * (dc - 1);
+            const int lo = max(dc == 0 ? 3 : 0, EDGE - X), hi = min(dc == fw - 1 ? 1 : 4, lg.detX1 - X);
+            s_cm[tid] = (uint8_t)(dc >= 0 && dc < fw && lo < hi ? (((1u << hi) - 1u) & ~((1u << lo) - 1u)) : 0u);
+        }
+#else
         if (tid < fw) {
             // dword column dc: pixels X .. X + 3, X = x0 + 4 (dc - 1); the ring columns contribute
             // the one pixel next to the tile, every pixel inside the detection region [16, detX1)
@@ -1910,6 +1930,7 @@ __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, G
             s_cm[dc] = (uint8_t)(lo < hi ? (((1u << hi) - 1u) & ~((1u << lo) - 1u)) : 0u);
         }
         if (tid >= fw && tid < fw + KF_DPL) s_cm[tid] = 0;  // the compass groups' dwords past the ring
+#endif
     }
     __syncthreads();
     KF_T(1);
@@ -1982,7 +2003,17 @@ __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, G
         // group k covers dwords KF_DPL k .. KF_DPL k + KF_DPL - 1 (those past the ring, fw ..,
         // have no detection pixel: s_cm is 0 there)
         int qn = 0;
+#if KF_B64
+        // group kp = dwords dc = 2 kp - 1, 2 kp (kp = 0: dc = -1 is a dummy with no detection
+        // pixel): with the tile's first staged byte sx = 16 or 24 (host: tile widths a multiple of
+        // 8 columns) every group's pair is 8-B aligned, so its row (and the left / right
+        // neighbours, up and down rows) are five ds_read_b64: a wave's 32-lane half reads 64
+        // consecutive dwords, conflict-free (the dword reads at an 8-B lane stride were 2-way
+        // bank conflicts: dword banks are (a / 4) mod 32, 64-bit reads' (a / 4) mod 64)
+        const int iw2 = t.sp >> 3, fwg = (fw >> 1) + 1;
+#else
         const int iw = t.sp >> 2, fwg = (fw + KF_DPL - 1) / KF_DPL;
+#endif
         const int prLo = max(0, EDGE + 1 - t.y0), prHi = min(t.th + 2, lg.detY1 + 1 - t.y0);  // wave-uniform
         const int nP = (prHi - prLo) * fwg;
         const int q256 = 256 / fwg, r256 = 256 - q256 * fwg;
@@ -1990,16 +2021,44 @@ __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, G
         int g = wave * 64 + lane;
         int pr = g / fwg, kp = g - pr * fwg;
         pr += prLo;
+#if KF_B64
+        int ad = (pr + 3) * t.sp + t.sx + 8 * kp - 8;  // byte offset of the group's first dword (dc = 2 kp - 1)
+        const int adSafe = 3 * t.sp + 16;
+#else
         int ad = (pr + 3) * t.sp + t.sx + 4 * (KF_DPL * kp - 1);  // byte offset of the group's first dword
         const int adSafe = 3 * t.sp + 4;
+#endif
         for (int it = wave; it * 64 < nP; it = __builtin_amdgcn_readfirstlane(it + 4)) {  // wave-uniform
             const bool valid = g < nP;
-            const uint32_t* row = (const uint32_t*)(s_in + (valid ? ad : adSafe));
             uint32_t h[KF_DPL + 2];  // dwords -1 .. KF_DPL of the group's row
+            uint32_t upv[KF_DPL], dnv[KF_DPL];
+#if KF_B64
+            const uint2* row2 = (const uint2*)(s_in + (valid ? ad : adSafe));
+            {
+                const uint2 L = row2[-1], C = row2[0], R = row2[1], U = row2[-3 * iw2], D = row2[3 * iw2];
+                h[0] = L.y;
+                h[1] = C.x;
+                h[2] = C.y;
+                h[3] = R.x;
+                upv[0] = U.x;
+                upv[1] = U.y;
+                dnv[0] = D.x;
+                dnv[1] = D.y;
+            }
+            const int dc = valid ? 2 * kp : fw + 1;  // s_cm index of the group's first dword (0 past the ring)
+            const int fq = pr * fw + 2 * kp - 1;
+#else
+            const uint32_t* row = (const uint32_t*)(s_in + (valid ? ad : adSafe));
 #pragma unroll
             for (int j = 0; j < KF_DPL + 2; ++j) h[j] = row[j - 1];
+#pragma unroll
+            for (int j = 0; j < KF_DPL; ++j) {
+                upv[j] = row[j - 3 * iw];
+                dnv[j] = row[j + 3 * iw];
+            }
             const int dc = valid ? KF_DPL * kp : fw;  // s_cm[fw ..] = 0: nothing queued
             const int fq = pr * fw + KF_DPL * kp;
+#endif
             // the row's dwords split once into even / odd byte lanes: a dword's q4 / q12 (pixels
             // x+3 / x-3) are the odd / even lanes of its neighbours, one v_alignbyte where they
             // straddle two dwords
@@ -2012,7 +2071,7 @@ __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, G
             uint32_t m[KF_DPL];
 #pragma unroll
             for (int j = 0; j < KF_DPL; ++j) {
-                const uint32_t up = row[j - 3 * iw], dn = row[j + 3 * iw];
+                const uint32_t up = upv[j], dn = dnv[j];
                 // even lanes (x, x+2): q4 = x+3, x+5 (odd bytes 3 / 1 of dwords 0 / +1), q12 = x-3, x-1
                 const uint32_t pe = compass_half(he[j + 1], even_bytes(dn), __builtin_amdgcn_alignbyte(ho[j + 2], ho[j + 1], 2),
                                                  even_bytes(up), ho[j], tt);
@@ -2399,18 +2458,41 @@ __global__ void __launch_bounds__(64 * OD_WAVES) k_orient_desc(const uint8_t* __
             q3 += (kOdRow[m + (m < 2)] - kOdRow[m]) / 2 * OD_HN;
         }
     }
-    float pat[16];  // pattern points 8*lane .. 8*lane+7 (tests 4*lane .. 4*lane+3): 4 float4 loads,
-                    // in flight across the second barrier
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const float4 f = ((const float4*)c_patternf)[lane * 4 + q];
-        pat[4 * q] = f.x;
-        pat[4 * q + 1] = f.y;
-        pat[4 * q + 2] = f.z;
-        pat[4 * q + 3] = f.w;
-    }
     lds_barrier();  // s_trig is written (and the row-pass sums: LDS)
     if (!active) return;
+    typedef float f32x2v __attribute__((ext_vector_type(2)));
+    // The rBRIEF pattern: points 8 lane .. 8 lane + 7 (tests 4 lane .. 4 lane + 3), pair q =
+    // (x, y) of point 8 lane + q.  The rule of DESIGN §6.1, as code: the loads are issued here,
+    // after the second barrier (no wave of the workgroup is in the row pass or the angle
+    // arithmetic any more), as eight fully coalesced dwordx2 rows of the pair-major table (512
+    // contiguous bytes per instruction, not the 64-B lane stride of the float4 form that returned
+    // wrong data), by one asm statement, and waited by another before the first sample (the
+    // registers are outputs of the first and in-out operands of the second: the compiler can
+    // neither move the loads nor read the registers early; the wave's setup below runs while
+    // they are in flight).  No other vector memory operation is issued between the two.
+#ifndef OD_PAT_SPLIT
+#define OD_PAT_SPLIT 1  // 0: the wait inside the issuing asm (441 vs 427 us c3 for the float4 form)
+#endif
+    f32x2v pat[8];
+    {
+        const uint32_t poff = 8u * (uint32_t)lane;
+        asm volatile(
+            "global_load_dwordx2 %0, %8, %9\n\t"
+            "global_load_dwordx2 %1, %8, %9 offset:512\n\t"
+            "global_load_dwordx2 %2, %8, %9 offset:1024\n\t"
+            "global_load_dwordx2 %3, %8, %9 offset:1536\n\t"
+            "global_load_dwordx2 %4, %8, %9 offset:2048\n\t"
+            "global_load_dwordx2 %5, %8, %9 offset:2560\n\t"
+            "global_load_dwordx2 %6, %8, %9 offset:3072\n\t"
+            "global_load_dwordx2 %7, %8, %9 offset:3584"
+#if !OD_PAT_SPLIT
+            "\n\ts_waitcnt vmcnt(0)"
+#endif
+            : "=&v"(pat[0]), "=&v"(pat[1]), "=&v"(pat[2]), "=&v"(pat[3]), "=&v"(pat[4]), "=&v"(pat[5]),
+              "=&v"(pat[6]), "=&v"(pat[7])
+            : "v"(poff), "s"((const float*)c_patternf)
+            : "memory");
+    }
     const float4 trig = s_trig[wave];
     const float angle = trig.x, a = trig.z, bsin = trig.y;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the row-pass sums are in LDS
@@ -2424,7 +2506,6 @@ __global__ void __launch_bounds__(64 * OD_WAVES) k_orient_desc(const uint8_t* __
     // rounding, exact for |v| < 2^22; the even addend keeps the tie parity), so the bits are
     // kMagic + dy + 18 = kMagic + r0 (window row of the first tap) and kMagic + dx + 18.
     constexpr uint32_t kMagic = 0x4B400000u;
-    typedef float f32x2v __attribute__((ext_vector_type(2)));
     const f32x2v rA = {a, -bsin}, rB = {bsin, a};
     // tap words of the column pass for even / odd r0, opaque so they stay in VGPRs
     uint32_t tE0 = GP_E0, tE1 = GP_E1, tE2 = GP_E2, tE3 = GP_E3;
@@ -2436,14 +2517,25 @@ __global__ void __launch_bounds__(64 * OD_WAVES) k_orient_desc(const uint8_t* __
     const uint32_t thr = kMagic + 18u + (uint32_t)(lg.xsimd_blur - x);
     uint32_t bxs[8], bys[8];
     int vals[8];
+#if OD_PAT_SPLIT
+    asm volatile("s_waitcnt vmcnt(0)"
+                 : "+v"(pat[0]), "+v"(pat[1]), "+v"(pat[2]), "+v"(pat[3]), "+v"(pat[4]), "+v"(pat[5]), "+v"(pat[6]),
+                   "+v"(pat[7])::"memory");
+#endif
     // one copy of the loop per wave-uniform tail case (no per-sample tail test when none)
     auto samples = [&](auto tailC) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-        const f32x2v pyv = {pat[2 * q + 1], pat[2 * q + 1]}, pxv = {pat[2 * q], pat[2 * q]};
+        // R = (fma(px, b, py * a), fma(px, a, py * -b)) with px / py splat from the loaded pair
+        // by op_sel (no copies): v_pk_mul_f32 takes py (the high half) for both lanes, v_pk_fma_f32
+        // px (the low half) for both
+        f32x2v R;
+        asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+            "v_pk_fma_f32 %0, %1, %3, %0 op_sel:[0,0,0] op_sel_hi:[0,1,1]"
+            : "=&v"(R)
+            : "v"(pat[q]), "v"(rA), "v"(rB));
         // (the magic add per element: this compiler turns a <2 x float> add of a splat literal
         // into the low lane's sum copied to both lanes)
-        const f32x2v R = __builtin_elementwise_fma(pxv, rB, pyv * rA);
         const uint32_t by = __builtin_bit_cast(uint32_t, R.x + 12582930.0f);
         const uint32_t bx = __builtin_bit_cast(uint32_t, R.y + 12582930.0f);
         bxs[q] = bx;
@@ -2621,7 +2713,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
     // y = the F2 keypoint index — one LDS read gives the greedy pass all it needs of a slot
     uint32_t* s_d2;
     uint2* s_st;
-    float *s_x2, *s_y2, *s_qx, *s_qy, *s_a2, *s_a1 = nullptr;
+    float *s_x2, *s_y2, *s_qx, *s_qy, *s_a2, *s_qa = nullptr;
     int *s_cell, *s_q2i, *s_lcnt, *s_m12;
     uint32_t* s_list;
     short* s_bslot;
@@ -2635,11 +2727,11 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
         s_qx = (float*)(s_q2i + nmax);
         s_qy = s_qx + nmax;
         s_a2 = s_qy + nmax;                       // F2 slot angle
-        s_list = (uint32_t*)(s_a2 + nmax);        // nmax x TOPK
+        s_qa = s_a2 + nmax;                       // query angle (the F1 keypoint's)
+        s_list = (uint32_t*)(s_qa + nmax);        // nmax x TOPK
         s_lcnt = (int*)(s_list + (size_t)nmax * MATCH_TOPK);
         s_m12 = s_lcnt + nmax;                    // vnMatches12 (cap)
         s_bslot = (short*)(s_m12 + cap);          // F2 slot of each accepted i1 (cap)
-        s_a1 = (float*)(s_bslot + ((cap + 1) & ~1));  // F1 query angles by keypoint index (cap)
     } else {
         s_st = (uint2*)smem;                      // LDS: greedy state
         s_m12 = (int*)(s_st + nmax);
@@ -2719,7 +2811,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
         const orb_keypoint_t kp = K1[i1];
         s_qx[q] = prev ? prev[((long long)p * cap + i1) * 2] : kp.x;
         s_qy[q] = prev ? prev[((long long)p * cap + i1) * 2 + 1] : kp.y;
-        if constexpr (!BIG) s_a1[i1] = kp.angle;  // (only queries are ever accepted)
+        if constexpr (!BIG) s_qa[q] = kp.angle;  // (only queries are ever accepted)
     }
     if constexpr (BIG) __threadfence_block();
     __syncthreads();
@@ -2934,12 +3026,15 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
     if (A.checkOri) {
         if (tid < 32) s_hist[tid] = 0;
         __syncthreads();
-        // rotation bin of every accepted i1, the stolen ones included (ORBmatcher.cc:664-676); the
-        // angles from LDS (s_a1 / s_a2), the slot kept for the output pass
-        for (int i = tid; i < n1; i += NT) {
+        // rotation bin of every accepted i1, the stolen ones included (ORBmatcher.cc:664-676); only
+        // queries are ever accepted, so the LDS body walks its queries (angles from LDS: s_qa /
+        // s_a2, the slot kept for the output pass); the histogram is a count, so order is free
+        const int nw = BIG ? n1 : n1c;
+        for (int t = tid; t < nw; t += NT) {
+            const int i = BIG ? t : s_q2i[t];
             const int sl = s_bslot[i];
             if (sl < 0) continue;
-            atomicAdd(&s_hist[rot_bin30((BIG ? K1[i].angle : s_a1[i]) - s_a2[sl])], 1);
+            atomicAdd(&s_hist[rot_bin30((BIG ? K1[i].angle : s_qa[t]) - s_a2[sl])], 1);
         }
         __syncthreads();
         if (tid == 0) {  // ComputeThreeMaxima (ORBmatcher.cc:1748-1789)
@@ -2975,10 +3070,11 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
         }
         __syncthreads();
         const int i1x = s_ind[0], i2x = s_ind[1], i3x = s_ind[2];
-        for (int i = tid; i < n1; i += NT) {
+        for (int t = tid; t < nw; t += NT) {
+            const int i = BIG ? t : s_q2i[t];
             const int sl = s_bslot[i];
             if (sl < 0) continue;
-            const int bn = rot_bin30((BIG ? K1[i].angle : s_a1[i]) - s_a2[sl]);
+            const int bn = rot_bin30((BIG ? K1[i].angle : s_qa[t]) - s_a2[sl]);
             if (bn != i1x && bn != i2x && bn != i3x) s_m12[i] = -1;
         }
         __syncthreads();
@@ -3492,9 +3588,19 @@ struct orb_extractor {
         for (int l = 0; l < nlevels; ++l) {
             const int detW = G.lv[l].detX1 - orbdev::EDGE;
             const int nx = (detW + FT_TW_MAX - 1) / FT_TW_MAX;
-            const int tw4 = std::max(2, ((detW + 3) / 4 + nx - 1) / nx), TW = 4 * tw4;
+            int tw4 = std::max(2, ((detW + 3) / 4 + nx - 1) / nx);
+#if KF_B64
+            tw4 = (tw4 + 1) & ~1;  // tiles of a multiple of 8 columns: every x0 = 0 mod 8
+#endif
+            const int TW = 4 * tw4;
             for (int x0 = orbdev::EDGE; x0 < G.lv[l].detX1; x0 += TW) {
+#if KF_B64
+                // first staged byte at sx = 16 + (x0 mod 16) in {16, 24}: the compass groups' dword
+                // pairs (sx - 8 + 8 kp) 8-B aligned, and 16 bytes left of the tile for the left pair
+                const int sx = 16 + (x0 & 15);
+#else
                 const int sx = x0 - (((x0 + orbdev::EDGE - 8) & ~15) - orbdev::EDGE);
+#endif
                 const int sp = (sx + TW + 8 + 15) & ~15, spw = TW + 8;
                 const int thMax = std::min({FT_IN_BYTES / sp - 8, FT_S_BYTES / spw - 2, 126, 4095 / (tw4 + 2) - 2});
                 if (thMax < 1 || sp > 288) return set_err(ORB_EINVAL, "k_fast tile geometry");
@@ -3984,6 +4090,12 @@ struct orb_extractor {
         }
         // (the frames' per-level output offsets and totals: written by each frame's last k_select
         // workgroup, select_frame_done)
+        if (hipError_t e = hipGetLastError(); e != hipSuccess) {
+            // a k_select launch that did not run to completion leaves selDone[b] counting: clear it,
+            // or the next extraction on this handle would take its frames' counts from stale levels
+            (void)hipMemsetAsync(d_selDone, 0, (size_t)maxBatch * sizeof(int), st);
+            return set_err(ORB_EDEVICE, std::string("k_select launch: ") + hipGetErrorString(e));
+        }
         stage_end(3, st);
         stage_begin(4, st);
         dim3 gd((std::max(kpCap, 1) + OD_WAVES - 1) / OD_WAVES, B);
@@ -4000,9 +4112,10 @@ static int upload_pattern(int device) {
     static std::mutex mu;
     std::lock_guard<std::mutex> lock(mu);
     if (device >= 0 && device < 64 && uploaded[device]) return ORB_OK;
-    HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), kOrbPattern31, sizeof(kOrbPattern31)));
-    float pf[1024];
-    for (int i = 0; i < 1024; ++i) pf[i] = (float)kOrbPattern31[i];
+    float pf[1024];  // pair-major: point 8 l + q at pair 64 q + l (c_patternf)
+    for (int l = 0; l < 64; ++l)
+        for (int q = 0; q < 8; ++q)
+            for (int c = 0; c < 2; ++c) pf[2 * (64 * q + l) + c] = (float)kOrbPattern31[2 * (8 * l + q) + c];
     HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_patternf), pf, sizeof(pf)));
     {  // IC disc masks per alignment (umax of ORBextractor.cc:495-510, HALF_PATCH_SIZE 15)
         int um[16];
@@ -4283,9 +4396,9 @@ int orb_descriptor_distance(const uint8_t* a, const uint8_t* b) {
 #define MATCH_NMAX_MIN 256
 #endif
 static size_t match_lds_bytes(int cap, int nmax) {
-    // F2 slots (desc 32 + state 8 + x,y,a,cell 16) + queries (q2i,qx,qy 12 + top-8 32 + cnt 4)
-    // + cap x (m12 4 + slot 2 + query angle 4)
-    return (size_t)nmax * (56 + 48) + (size_t)cap * 10 + 32;
+    // F2 slots (desc 32 + state 8 + x,y,a,cell 16) + queries (q2i,qx,qy,angle 16 + top-8 32 +
+    // cnt 4) + cap x (m12 4 + slot 2): nmax 1024 and cap 8192 fit (156 KB)
+    return (size_t)nmax * (56 + 52) + (size_t)cap * 6 + 32;
 }
 static size_t match_big_lds_bytes(int cap, int nmax) { return (size_t)nmax * 8 + (size_t)cap * 6 + 16; }
 

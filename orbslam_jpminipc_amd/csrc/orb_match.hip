@@ -706,8 +706,11 @@ __global__ void __launch_bounds__(256) k_resolve(Job J) {
     const int Tn = J.T.n;
     constexpr int m = MODE;
     int* s_out = (int*)smem;                                  // outN
-    int* s_acc = s_out + J.outN;                               // accepted: (slot << 5) | bin
-    uint8_t* s_taken = (uint8_t*)(s_acc + max(Tn, 1));          // Tn
+    // accepted matches in acceptance order: (slot << 5) | bin and the partner (the other index of
+    // the pair, as accepted: a slot accepted twice keeps both pairs' bins, as rotHist does)
+    int* s_acc = s_out + J.outN;                               // Tn (an acceptance takes a target)
+    int* s_accp = s_acc + max(Tn, 1);                          // Tn
+    uint8_t* s_taken = (uint8_t*)(s_accp + max(Tn, 1));         // Tn
     for (int i = tid; i < J.outN; i += 256) s_out[i] = -1;
     for (int i = tid; i < Tn; i += 256) s_taken[i] = J.taken0 ? J.taken0[i] : 0;
     if (tid == 0) s_nacc = 0;
@@ -836,7 +839,10 @@ __global__ void __launch_bounds__(256) k_resolve(Job J) {
                         const int qv = qrow(J, q);
                         const int slot = J.outByTarget ? bestIdx : qv;
                         s_out[slot] = J.outByTarget ? qv : bestIdx;
-                        if (rotMode) s_acc[nacc] = slot << 5;  // its rotation bin: after the pass, in parallel
+                        if (rotMode) {  // its rotation bin: after the pass, in parallel
+                            s_acc[nacc] = slot << 5;
+                            s_accp[nacc] = J.outByTarget ? qv : bestIdx;
+                        }
                     }
                     ++nacc;
                     // lane 0's LDS writes land before any lane's next read (same wave, in order)
@@ -888,8 +894,15 @@ __global__ void __launch_bounds__(256) k_resolve(Job J) {
                         // lane 8g + k checks group k's accepted target against query g's best / second
                         const int bIdxK = __shfl(bIdx, 8 * cand, 64);
                         // (best-only matchers: the second does not decide, so only the best can be hit)
+                        // KF-KF over a non-unique FeatureVector: two queries of the batch may be one
+                        // keypoint row (output slot); the later one must see the earlier's commit
+                        bool sameRow = false;
+                        if constexpr (m == M_BOW_KFKF) {
+                            const int qvG = qrow(J, c * RES_CHUNK + jg);
+                            sameRow = __shfl(qvG, 8 * cand, 64) == qvG;
+                        }
                         const bool hit = cand < grp && ((accW >> (8 * cand)) & 1ull) &&
-                                         (bIdxK == bIdx || (need == 2 && bIdxK == sIdx));
+                                         (bIdxK == bIdx || (need == 2 && bIdxK == sIdx) || sameRow);
                         const uint64_t stopM = __ballot(grp < nb && (hit || (rescan && cand == 0)));
                         const int jstop = stopM ? (__ffsll((unsigned long long)stopM) - 1) >> 3 : nb;
                         if (accept && cand == 0 && grp < jstop) {
@@ -902,6 +915,7 @@ __global__ void __launch_bounds__(256) k_resolve(Job J) {
                                 // rank among the batch's committed acceptances: query order kept
                                 const uint64_t before = accW & ((1ull << (8 * grp)) - 1ull);
                                 s_acc[nacc + __popcll(before)] = slot << 5;
+                                s_accp[nacc + __popcll(before)] = J.outByTarget ? qv : bIdx;
                             }
                         }
                         nacc += __popcll(accW & (jstop >= 8 ? ~0ull : ((1ull << (8 * jstop)) - 1ull)));
@@ -926,7 +940,7 @@ __global__ void __launch_bounds__(256) k_resolve(Job J) {
         if (tid < HISTO) s_hist[tid] = 0;
         __syncthreads();
         for (int i = tid; i < nacc; i += 256) {
-            const int slot = s_acc[i] >> 5, v = s_out[slot];
+            const int slot = s_acc[i] >> 5, v = s_accp[i];
             const int qv = J.outByTarget ? v : slot, ti = J.outByTarget ? slot : v;
             const int bin = rot_bin(J.qkps[qv].angle, J.T.kps[ti].angle);
             s_acc[i] = (slot << 5) | bin;
@@ -1257,7 +1271,7 @@ void bind_job(const Call& C, Job& J, const JobOffs& o, int qn, int outN) {
 }
 
 int resolve_lds(const Job& J, size_t* bytes) {
-    *bytes = (size_t)J.outN * 4 + (size_t)std::max(J.T.n, 1) * 4 + (size_t)J.T.n + 16;
+    *bytes = (size_t)J.outN * 4 + (size_t)std::max(J.T.n, 1) * 8 + (size_t)J.T.n + 16;
     if (*bytes > 150 * 1024) return fail(ORB_ENOTSUP, "matcher state exceeds LDS (too many keypoints/queries)");
     return ORB_OK;
 }

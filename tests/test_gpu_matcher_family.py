@@ -254,6 +254,25 @@ def test_search_by_bow_kf_kf(seed):
         assert n > 0
 
 
+@pytest.mark.parametrize("seed", range(2))
+@pytest.mark.parametrize("n_pts,extra", [(2000, 400), (3200, 900)])
+def test_search_by_bow_large_frames(seed, n_pts, extra):
+    """Keyframes of 2400 / 4100 features (the init extractor's 2000-feature frames and
+    beyond): k_bow_pairs runs its unstaged template (the frames' descriptors no longer fit
+    its LDS), KF-F and KF-KF, with usable flags and both checkOri settings."""
+    rng = np.random.default_rng(1400 + 10 * seed + n_pts)
+    V1, V2, fv1, fv2 = _bow_pair(rng, n_pts=n_pts, extra=extra)
+    assert V1.n >= 2000 and V2.n >= 2000
+    u1 = (rng.random(V1.n) < 0.8).astype(np.uint8)
+    u2 = (rng.random(V2.n) < 0.8).astype(np.uint8)
+    for nn, co in ((0.75, True), (0.9, False)):
+        g, o = both(nn, co)
+        n = same(g.SearchByBoW_KF_F(V1, u1, fv1, V2, fv2), o.SearchByBoW_KF_F(V1, u1, fv1, V2, fv2))
+        assert n > 0
+        n = same(g.SearchByBoW_KF_KF(V1, u1, fv1, V2, u2, fv2), o.SearchByBoW_KF_KF(V1, u1, fv1, V2, u2, fv2))
+        assert n > 0
+
+
 @pytest.mark.parametrize("seed", SEEDS)
 def test_search_for_triangulation(seed):
     rng = np.random.default_rng(1300 + seed)
@@ -292,6 +311,34 @@ def test_dense_contention_forces_rescans():
     n = same(g.SearchByBoW_KF_KF(F1, None, fv1, F2, None, fv2), o.SearchByBoW_KF_KF(F1, None, fv1, F2, None, fv2))
     n = same(g.SearchByBoW_KF_F(F1, None, fv1, F2, fv2), o.SearchByBoW_KF_F(F1, None, fv1, F2, fv2))
     assert n > 8
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_bow_non_unique_feature_vectors(seed):
+    """FeatureVectors listing a feature under two nodes (transform never produces them, the
+    reference's loops accept them): the generic resolver decides query by query, a keypoint
+    row accepted twice keeps both pairs' rotation bins (rotHist entries), and two queries of
+    one speculative batch that share a row are not committed together."""
+    rng = np.random.default_rng(1500 + seed)
+    V1, V2, _, _ = _bow_pair(rng, n_pts=300, extra=60)
+    nn = 24
+    a1 = rng.integers(0, nn, V1.n)
+    a2 = rng.integers(0, nn, V2.n)
+    d1 = {k: [] for k in range(nn)}
+    for i in range(V1.n):
+        d1[int(a1[i])].append(i)
+        d1[int((a1[i] + 1 + rng.integers(0, 3)) % nn)].append(i)
+    d2 = {k: [] for k in range(nn)}
+    for i in range(V2.n):
+        d2[int(a2[i])].append(i)
+        if rng.random() < 0.3:
+            d2[int((a2[i] + 5) % nn)].append(i)
+    fv1 = S.FeatureVector.from_dict({k: sorted(v) for k, v in d1.items() if v})
+    fv2 = S.FeatureVector.from_dict({k: sorted(v) for k, v in d2.items() if v})
+    for nnr, co in ((0.9, True), (0.75, True), (0.9, False)):
+        g, o = both(nnr, co)
+        same(g.SearchByBoW_KF_KF(V1, None, fv1, V2, None, fv2), o.SearchByBoW_KF_KF(V1, None, fv1, V2, None, fv2))
+        same(g.SearchByBoW_KF_F(V1, None, fv1, V2, fv2), o.SearchByBoW_KF_F(V1, None, fv1, V2, fv2))
 
 
 def test_empty_inputs():

@@ -70,6 +70,19 @@ def test_sfi_random_pairs(seed, n1, n2):
     assert _run_both(k1, d1, k2, d2) > 0
 
 
+@pytest.mark.parametrize("n1,n2,p0", [(5800, 6000, 0.15), (8192, 8192, 0.12), (8192, 7000, 0.6)])
+def test_sfi_large_capacity(n1, n2, p0):
+    """Frames of up to 8192 keypoints (the ABI's limit): with few octave-0 keypoints the
+    LDS body runs at that capacity (its per-keypoint LDS arrays sized by cap), with many
+    the large-capacity body; neither may refuse the call (ORB_ENOTSUP)."""
+    rng = np.random.default_rng(n1 + n2)
+    k1, k2 = _kps(rng, n1, p0=p0), _kps(rng, n2, p0=p0)
+    base = rng.integers(0, 256, (64, 32), dtype=np.uint8)  # shared bases: real candidates
+    d1 = _flip(rng, base[rng.integers(0, 64, n1)], 12)
+    d2 = _flip(rng, base[rng.integers(0, 64, n2)], 12)
+    assert _run_both(k1, d1, k2, d2, 0.9, True, 40) > 0
+
+
 @pytest.mark.parametrize("pool", [1, 3, 8, 32])
 @pytest.mark.parametrize("nnratio,checkOri,window", [(0.9, True, 100), (1.0, False, 200), (0.6, True, 40)])
 def test_sfi_descriptor_pool_conflicts(pool, nnratio, checkOri, window):
