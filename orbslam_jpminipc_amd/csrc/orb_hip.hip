@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "../../include/orb_abi.h"
+#include "../../include/orb_debug.h"
 #include "nth_select.h"
 #include "orb_internal.h"
 #include "orb_device.h"
@@ -2511,8 +2512,11 @@ __global__ void __launch_bounds__(64 * OD_WAVES) k_orient_desc(const uint8_t* __
     uint32_t tE0 = GP_E0, tE1 = GP_E1, tE2 = GP_E2, tE3 = GP_E3;
     uint32_t tO0 = GP_O0, tO1 = GP_O1, tO2 = GP_O2, tO3 = GP_O3;
     asm volatile("" : "+v"(tE0), "+v"(tE1), "+v"(tE2), "+v"(tE3), "+v"(tO0), "+v"(tO1), "+v"(tO2), "+v"(tO3));
-    // sum (pair p, column dx + 18 + o0) = hbase[56 p + bits_x] (32-bit LDS addresses wrap)
-    const uint32_t* hbase = Hs + (o0 - (int)kMagic);
+    // sum (pair p, column dx + 18 + o0) = hbase[56 p + bits_x] (32-bit LDS addresses wrap); the
+    // pair index p = r0 >> 1 comes from v_mul_u32_u24 of by >> 1, whose low 24 bits are
+    // ((kMagic >> 1) & 0xFFFFFF) + p: that constant is taken off the base
+    const uint32_t* hbase = Hs + (o0 - (int)kMagic) - (int)(OD_HN * ((kMagic >> 1) & 0xFFFFFFu));
+    const uint32_t hb = (uint32_t)((const uint8_t*)hbase - s_buf[0]);  // as a byte offset from s_buf
     // tail columns (scalar-tail rounding): x + dx >= xsimd_blur <=> bits_x >= thr
     const uint32_t thr = kMagic + 18u + (uint32_t)(lg.xsimd_blur - x);
     uint32_t bxs[8], bys[8];
@@ -2540,7 +2544,11 @@ __global__ void __launch_bounds__(64 * OD_WAVES) k_orient_desc(const uint8_t* __
         const uint32_t bx = __builtin_bit_cast(uint32_t, R.y + 12582930.0f);
         bxs[q] = bx;
         bys[q] = by;
-        const uint32_t* hq = hbase + (int)(__umul24(__builtin_amdgcn_ubfe(by, 1, 8), OD_HN) + bx);
+        // byte offset (by >> 1) * 224 + 4 bx: v_lshl_add_u32 + v_mad_u32_u24 (the compiler's
+        // mul / shift / add3 was one more)
+        uint32_t hoff;
+        asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(hoff) : "v"(by >> 1), "v"(4u * OD_HN), "v"((bx << 2) + hb));
+        const uint32_t* hq = (const uint32_t*)(s_buf[0] + hoff);
         // odd r0: the first pair starts one row early (taps shifted by one u16 lane)
         const uint32_t om = (uint32_t)__builtin_amdgcn_sbfe((int)by, 0, 1);
         const uint32_t t0 = bfi(om, tO0, tE0), t1 = bfi(om, tO1, tE1);

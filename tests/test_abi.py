@@ -26,6 +26,11 @@ def exported(so: pathlib.Path):
 def test_hip_library_exports_every_abi_symbol():
     names = declared_functions(ROOT / "include" / "orb_abi.h")
     assert "orb_extract" in names and "orb_search_for_initialization_batch_device" in names
+    # the test / diagnostic hooks live in their own header, outside the reference-facing ABI
+    debug = declared_functions(ROOT / "include" / "orb_debug.h")
+    assert debug and all(n.startswith("orb_debug_") for n in debug)
+    assert not [n for n in names if n.startswith("orb_debug_")]
+    names = names + debug
     lib = orb.hip_lib()
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
