@@ -27,6 +27,7 @@
 #include <mutex>
 #include <string>
 #include <type_traits>
+#include <chrono>
 #include <vector>
 
 #include "../../include/orb_abi.h"
@@ -149,6 +150,13 @@ struct CellGeom {
 // kernels
 // ======================================================================================
 using namespace orbdev;
+
+// (m & a) | (~m & b) in one VALU
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
+    return r;
+}
 
 // bit_pattern_31_ (ORBextractor.cc:197-455) as floats, pair-major: c_patternf[2 (64 q + l) + {0, 1}]
 // = (x, y) of point 8 l + q, i.e. lane l's eight points are one float2 in each of eight 512-B
@@ -326,6 +334,7 @@ __global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, c
     uint32_t o0[4], o1[4], a0[4], a1[4];
     uint32_t liveMask = 0;
     bool allSimd = true;
+    uint32_t simdBytes = 0;  // 0xFF in the byte of every SSE2 column
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int px = x4 + i;
@@ -343,9 +352,14 @@ __global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, c
         o0[i] = (uint32_t)(sx - colStart);
         o1[i] = (uint32_t)((a1[i] ? sx + 1 : sx) - colStart);
         allSimd = allSimd && lx < lg.xs_resize;
+        if (lx < lg.xs_resize) simdBytes |= 0xFFu << (8 * i);
     }
     __syncthreads();
     if (x4 >= lg.pitch) return;
+    // a wave holding a scalar-tail column computes both formulas for all its lanes and selects per
+    // byte (wave-uniform: no divergent path per row); the other waves the SSE2 one alone
+    const bool waveTail = __ballot(!allSimd) != 0ull;
+    const bool shift4 = allSimd && !waveTail;
     const uint8_t* L = (const uint8_t*)s_src;
     const int LP = words * 16;
     // horizontal sums of source row r: H >> 4 on the SSE2 columns, H on the scalar tail
@@ -353,7 +367,7 @@ __global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, c
         const uint8_t* R = L + (r - rowMin) * LP;
 #pragma unroll
         for (int i = 0; i < 4; ++i) h[i] = (uint32_t)R[o0[i]] * a0[i] + (uint32_t)R[o1[i]] * a1[i];
-        if (allSimd) {
+        if (shift4) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) h[i] >>= 4;
         }
@@ -363,24 +377,20 @@ __global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, c
     auto vrow = [&](const int py, const uint32_t bb, const uint32_t* hA, const uint32_t* hB) {
         const uint32_t b0 = bb & 0xFFFFu, b1 = bb >> 16;
         uint32_t word;
-        if (allSimd) {
+        if (!waveTail) {
             const uint32_t B0 = b0 << 16, B1 = b1 << 16;
             uint32_t r[4];
 #pragma unroll
             for (int i = 0; i < 4; ++i) r[i] = (__umulhi(hA[i], B0) + __umulhi(hB[i], B1) + 2u) >> 2;
             word = r[0] | (r[1] << 8) | (r[2] << 16) | (r[3] << 24);
-        } else {  // lanes holding a column of the scalar tail (hA / hB are full sums)
-            word = 0;
+        } else {  // hA / hB are full sums in this wave
+            uint32_t ws = 0, wc = 0;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const int lx = reflect101(min(x4 + i, lg.w + 2 * EDGE - 1) - EDGE, lg.w);
-                uint32_t r;
-                if (lx < lg.xs_resize)
-                    r = (__umulhi(hA[i] >> 4, b0 << 16) + __umulhi(hB[i] >> 4, b1 << 16) + 2u) >> 2;
-                else
-                    r = (hA[i] * b0 + hB[i] * b1 + (1u << 21)) >> 22;
-                word |= r << (8 * i);
+                ws |= ((__umulhi(hA[i] >> 4, b0 << 16) + __umulhi(hB[i] >> 4, b1 << 16) + 2u) >> 2) << (8 * i);
+                wc |= ((hA[i] * b0 + hB[i] * b1 + (1u << 21)) >> 22) << (8 * i);
             }
+            word = bfi(simdBytes, ws, wc);
         }
         *(uint32_t*)(D + (long long)py * lg.pitch) = word & liveMask;
     };
@@ -694,6 +704,7 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
         uint32_t simd;
         bool allSimd;
         uint32_t hmask;
+        uint32_t simdBytes;  // 0xFF in the byte of every SSE2 column (the others: the scalar tail)
     };
     auto decode_quad = [&](const uint4 cw) {
         // column words: sx | a1 << 12 | (a0 - 2047 + a1) << 24 | simd << 26 | live << 27
@@ -701,12 +712,13 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
         const uint32_t cc[4] = {cw.x, cw.y, cw.z, cw.w};
         Q.live = 0;
         Q.simd = 0;
+        Q.simdBytes = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             Q.sx[j] = (int)(cc[j] & 0xFFFu);
             const uint32_t a1 = (cc[j] >> 12) & 0xFFFu;
             Q.ap[j] = (2047u + ((cc[j] >> 24) & 3u) - a1) | (a1 << 16);
-            if (cc[j] & (1u << 26)) Q.simd |= 1u << j;
+            if (cc[j] & (1u << 26)) Q.simd |= 1u << j, Q.simdBytes |= 0xFFu << (8 * j);
             if (cc[j] & (1u << 27)) Q.live |= 0xFFu << (8 * j);
         }
         Q.allSimd = Q.simd == 0xFu;
@@ -716,8 +728,13 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
     auto build_quad = [&](const int q, const QuadCols& Q, const uint4* E, const int cnt) {
         const int* sx = Q.sx;
         const uint32_t* ap = Q.ap;
-        const uint32_t live = Q.live, simd = Q.simd, hmask = Q.hmask;
+        const uint32_t live = Q.live, hmask = Q.hmask;
         const bool allSimd = Q.allSimd;
+        // the level's scalar-tail columns (VResizeLinear's columns past the SSE2 body: one or two
+        // quads per level) make their wave take the mixed path below for every row; the other
+        // waves run the all-SSE2 formula alone (wave-uniform: no divergent path per row)
+        const bool waveTail = __ballot(!allSimd) != 0ull;
+        const uint32_t simdBytes = Q.simdBytes;
         // HResizeLinear of the source row at LDS address `ra`: H = S[sx] a0 + S[sx+1] a1
         // (a1 == 0 where OpenCV reads S[sx] only: the byte after it is multiplied by 0; it
         // lies in the ring row's slack or the next LDS row, never outside the allocation).
@@ -742,21 +759,25 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
         // one output row from its two source rows' horizontal sums hA (row s0) and hB (row s1)
         auto vrow = [&](const uint4 e0, const uint4 e1, const uint32_t* hA, const uint32_t* hB) {
             uint32_t word = 0;
-            if (allSimd) {
+            if (!waveTail) {
                 // VResizeLinearVec_32s8u: ((H >> 4) * b) >> 16 per term = the high 32 bits of
                 // (H & ~15) * (b << 12) (both < 2^24), + 2 >> 2
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
                     word |= ((mulhi24(hA[j], e0.z) + mulhi24(hB[j], e0.w) + 2u) >> 2) << (8 * j);
             } else {
+                // both formulas for every column, the byte per column by one v_bfi (the branchy
+                // per-column select cost the tail's wave both paths every row: k_pyr_stream 316 ->
+                // 284 us c3 without it, timing-only ablation): SSE2 on H & ~15 (a tail quad's sums
+                // are unmasked), the scalar VResizeLinear (H0 b0 + H1 b1 + 2^21) >> 22 on H
                 const uint32_t b0 = e0.z >> 12, b1 = e0.w >> 12;
+                uint32_t ws = 0, wc = 0;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const uint32_t r = ((simd >> j) & 1u)
-                                           ? ((__umul24(hA[j] >> 4, b0) >> 16) + (__umul24(hB[j] >> 4, b1) >> 16) + 2u) >> 2
-                                           : (__umul24(hA[j], b0) + __umul24(hB[j], b1) + (1u << 21)) >> 22;
-                    word |= r << (8 * j);
+                    ws |= ((mulhi24(hA[j] & ~15u, e0.z) + mulhi24(hB[j] & ~15u, e0.w) + 2u) >> 2) << (8 * j);
+                    wc |= ((__umul24(hA[j], b0) + __umul24(hB[j], b1) + (1u << 21)) >> 22) << (8 * j);
                 }
+                word = bfi(simdBytes, ws, wc);
             }
             word &= live;
             // wave-uniform row base (SGPRs) + the lane's 32-bit offset: no 64-bit VALU address
@@ -2281,12 +2302,6 @@ __device__ __forceinline__ uint32_t vpass(const uint32_t* __restrict__ Hs, int r
     return dot2u(h3, t3, dot2u(h2, t2, dot2u(h1, t1, dot2u(h0, t0, 0u))));
 }
 
-// (m & a) | (~m & b) in one VALU
-__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {
-    uint32_t r;
-    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b));
-    return r;
-}
 
 // cvRound-equivalent of T / 65536: half to even (SSE2 columns) or half up (scalar tail), then
 // the saturating cast.
@@ -2459,23 +2474,24 @@ __global__ void __launch_bounds__(64 * OD_WAVES) k_orient_desc(const uint8_t* __
             q3 += (kOdRow[m + (m < 2)] - kOdRow[m]) / 2 * OD_HN;
         }
     }
-    lds_barrier();  // s_trig is written (and the row-pass sums: LDS)
-    if (!active) return;
     typedef float f32x2v __attribute__((ext_vector_type(2)));
     // The rBRIEF pattern: points 8 lane .. 8 lane + 7 (tests 4 lane .. 4 lane + 3), pair q =
-    // (x, y) of point 8 lane + q.  The rule of DESIGN §6.1, as code: the loads are issued here,
-    // after the second barrier (no wave of the workgroup is in the row pass or the angle
-    // arithmetic any more), as eight fully coalesced dwordx2 rows of the pair-major table (512
-    // contiguous bytes per instruction, not the 64-B lane stride of the float4 form that returned
-    // wrong data), by one asm statement, and waited by another before the first sample (the
-    // registers are outputs of the first and in-out operands of the second: the compiler can
-    // neither move the loads nor read the registers early; the wave's setup below runs while
-    // they are in flight).  No other vector memory operation is issued between the two.
+    // (x, y) of point 8 lane + q.  The rule of DESIGN §6.1, as code: eight fully coalesced
+    // dwordx2 rows of the pair-major table (each instruction reads 512 contiguous bytes, four
+    // cache lines no other pattern load touches; the float4 form read all 32 lines of the table
+    // with each of its four instructions, 64-B lane stride, and returned wrong data), issued by
+    // one asm statement and waited by another before the first sample (the registers are outputs
+    // of the first and in-out operands of the second: the compiler can neither move the loads nor
+    // read the registers early).  OD_PAT_EARLY: issued by the active waves once their own row
+    // pass is done, in flight across the second barrier; else after it.
+#ifndef OD_PAT_EARLY
+#define OD_PAT_EARLY 1
+#endif
 #ifndef OD_PAT_SPLIT
 #define OD_PAT_SPLIT 1  // 0: the wait inside the issuing asm (441 vs 427 us c3 for the float4 form)
 #endif
     f32x2v pat[8];
-    {
+    auto issue_pattern = [&]() {
         const uint32_t poff = 8u * (uint32_t)lane;
         asm volatile(
             "global_load_dwordx2 %0, %8, %9\n\t"
@@ -2493,7 +2509,15 @@ __global__ void __launch_bounds__(64 * OD_WAVES) k_orient_desc(const uint8_t* __
               "=&v"(pat[6]), "=&v"(pat[7])
             : "v"(poff), "s"((const float*)c_patternf)
             : "memory");
-    }
+    };
+#if OD_PAT_EARLY
+    if (active) issue_pattern();
+#endif
+    lds_barrier();  // s_trig is written (and the row-pass sums: LDS)
+    if (!active) return;
+#if !OD_PAT_EARLY
+    issue_pattern();
+#endif
     const float4 trig = s_trig[wave];
     const float angle = trig.x, a = trig.z, bsin = trig.y;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the row-pass sums are in LDS
@@ -2678,6 +2702,8 @@ struct MatchArgs {
     int* m12out;
     int* nmOut;
     int P;
+    int* done;    // host call (P == 1): pinned flag the kernel sets to doneSeq once its outputs are
+    int doneSeq;  // visible to the host (the caller spins on it instead of a stream synchronisation)
 };
 
 // ORBmatcher.cc:664-670: the rotation's histogram bin (HISTO_LENGTH 30, factor 1/30)
@@ -2929,6 +2955,54 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
     // its queries before the first such one (their slots are distinct, their vnMatches21
     // predecessors precede the batch) and the next batch starts there.  A rescan query heading
     // a batch runs alone on the whole wave.
+    // the exact rescan of query q0's whole window, on all 64 lanes of wave 0 (a query whose
+    // truncated top-8 holds fewer than two live candidates)
+    auto rescan_query = [&](const int q0) {
+        const int i1 = s_q2i[q0];
+        const float qx = s_qx[q0], qy = s_qy[q0];
+        const int minCX = max(0, (int)floorf((qx - mg.minX - r) * mg.invW));
+        const int maxCX = min(63, (int)ceilf((qx - mg.minX + r) * mg.invW));
+        const int minCY = max(0, (int)floorf((qy - mg.minY - r) * mg.invH));
+        const int maxCY = min(47, (int)ceilf((qy - mg.minY + r) * mg.invH));
+        uint32_t d1[8];
+#pragma unroll
+        for (int w = 0; w < 2; ++w) {  // two 16-B loads (descriptor rows are 32-B aligned)
+            const uint4 v4 = ((const uint4*)D1)[(long long)i1 * 2 + w];
+            d1[4 * w] = v4.x, d1[4 * w + 1] = v4.y, d1[4 * w + 2] = v4.z, d1[4 * w + 3] = v4.w;
+        }
+        uint32_t lb = 0xFFFFFFFFu;
+        int ls = 0x7fffffff;
+        const int j1 = s_col[max(maxCX + 1, 0)];
+        for (int j = s_col[min(minCX, 64)] + lane; j < j1; j += 64) {
+            const int cell = s_cell[j];
+            const int cx = cell / 48, cy = cell - cx * 48;
+            if (cx < minCX || cx > maxCX || cy < minCY || cy > maxCY) continue;
+            if (fabsf(s_x2[j] - qx) > r || fabsf(s_y2[j] - qy) > r) continue;
+            const int dist = hamming256(d1, s_d2 + j * 8);
+            if ((int)(s_st[j].x & 0xFFFFu) <= dist) continue;
+            const uint32_t key = ((uint32_t)dist << KB) | (uint32_t)j;
+            if (key < lb) {
+                if (lb != 0xFFFFFFFFu) ls = (int)(lb >> KB);
+                lb = key;
+            } else if (dist < ls) {
+                ls = dist;
+            }
+        }
+        uint32_t gb = lb;
+        gb = wave_min_u32(gb);
+        int contrib = (lb == gb) ? ls : (lb == 0xFFFFFFFFu ? 0x7fffffff : (int)(lb >> KB));
+        contrib = (int)wave_min_u32((uint32_t)contrib);  // (non-negative)
+        if (gb == 0xFFFFFFFFu) return;
+        const int rDist = (int)(gb >> KB), rSlot = (int)(gb & SLOT);
+        if (rDist <= 50 && (float)rDist < (float)contrib * nnratio && lane == 0) {
+            const uint2 sb = s_st[rSlot];
+            const int old = (int)(sb.x >> 16) - 1;
+            if (old >= 0) s_m12[old] = -1;
+            s_m12[i1] = (int)(sb.y & 0x1FFFu);
+            s_st[rSlot].x = (uint32_t)rDist | ((uint32_t)(i1 + 1) << 16);
+            s_bslot[i1] = (short)rSlot;
+        }
+    };
     if (wave == 0 && n1c > 0) {
         const int grp = lane >> 3, cand = lane & 7;
         int q0 = 0;
@@ -2972,7 +3046,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
                 const int i1 = i1q;
                 const int old = (int)(st.x >> 16) - 1;  // vnMatches21[bestIdx2]
                 if (old >= 0) s_m12[old] = -1;
-                s_m12[i1] = (int)st.y;
+                s_m12[i1] = (int)(st.y & 0x1FFFu);
                 s_st[bestSlot].x = (uint32_t)bestDist | ((uint32_t)(i1 + 1) << 16);
                 s_bslot[i1] = (short)bestSlot;
             }
@@ -2980,52 +3054,8 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
                 q0 += jstop;
                 continue;
             }
-            // query q0 needs the exact rescan of its whole window, on all 64 lanes
-            const int i1 = s_q2i[q0];
-            const float qx = s_qx[q0], qy = s_qy[q0];
-            const int minCX = max(0, (int)floorf((qx - mg.minX - r) * mg.invW));
-            const int maxCX = min(63, (int)ceilf((qx - mg.minX + r) * mg.invW));
-            const int minCY = max(0, (int)floorf((qy - mg.minY - r) * mg.invH));
-            const int maxCY = min(47, (int)ceilf((qy - mg.minY + r) * mg.invH));
-            uint32_t d1[8];
-#pragma unroll
-            for (int w = 0; w < 2; ++w) {  // two 16-B loads (descriptor rows are 32-B aligned)
-                const uint4 v4 = ((const uint4*)D1)[(long long)i1 * 2 + w];
-                d1[4 * w] = v4.x, d1[4 * w + 1] = v4.y, d1[4 * w + 2] = v4.z, d1[4 * w + 3] = v4.w;
-            }
-            uint32_t lb = 0xFFFFFFFFu;
-            int ls = 0x7fffffff;
-            const int j1 = s_col[max(maxCX + 1, 0)];
-            for (int j = s_col[min(minCX, 64)] + lane; j < j1; j += 64) {
-                const int cell = s_cell[j];
-                const int cx = cell / 48, cy = cell - cx * 48;
-                if (cx < minCX || cx > maxCX || cy < minCY || cy > maxCY) continue;
-                if (fabsf(s_x2[j] - qx) > r || fabsf(s_y2[j] - qy) > r) continue;
-                const int dist = hamming256(d1, s_d2 + j * 8);
-                if ((int)(s_st[j].x & 0xFFFFu) <= dist) continue;
-                const uint32_t key = ((uint32_t)dist << KB) | (uint32_t)j;
-                if (key < lb) {
-                    if (lb != 0xFFFFFFFFu) ls = (int)(lb >> KB);
-                    lb = key;
-                } else if (dist < ls) {
-                    ls = dist;
-                }
-            }
-            uint32_t gb = lb;
-            gb = wave_min_u32(gb);
-            int contrib = (lb == gb) ? ls : (lb == 0xFFFFFFFFu ? 0x7fffffff : (int)(lb >> KB));
-            contrib = (int)wave_min_u32((uint32_t)contrib);  // (non-negative)
+            rescan_query(q0);
             q0 += 1;
-            if (gb == 0xFFFFFFFFu) continue;
-            const int rDist = (int)(gb >> KB), rSlot = (int)(gb & SLOT);
-            if (rDist <= 50 && (float)rDist < (float)contrib * nnratio && lane == 0) {
-                const uint2 sb = s_st[rSlot];
-                const int old = (int)(sb.x >> 16) - 1;
-                if (old >= 0) s_m12[old] = -1;
-                s_m12[i1] = (int)sb.y;
-                s_st[rSlot].x = (uint32_t)rDist | ((uint32_t)(i1 + 1) << 16);
-                s_bslot[i1] = (short)rSlot;
-            }
         }
     }
     __syncthreads();
@@ -3140,6 +3170,15 @@ __global__ void __launch_bounds__(NT) k_match_init(MatchArgs A, uint8_t* __restr
     if (match_pair<false, NT>(A, p, A.nmax, smem, nullptr) && big) {
         __syncthreads();  // the static LDS (counts, bins) is reused
         match_pair<true, NT>(A, p, nmaxBig, smem, big + (size_t)p * match_big_slot_bytes(A.cap, nmaxBig));
+    }
+    if (A.done) {  // (a host call's single workgroup) every wave's output stores complete, the
+                   // workgroup's writes made visible to the host (system-scope release), then the flag
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence_system();
+            __hip_atomic_store(A.done, A.doneSeq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
@@ -4477,11 +4516,11 @@ int orb_stream_destroy(void* stream) {
     return ORB_OK;
 }
 
-int orb_search_for_initialization_batch_device(const orb_keypoint_t* d_kps, const uint8_t* d_desc,
-                                               const int32_t* d_counts, int cap, int P, const int32_t* d_pair_f1,
-                                               const int32_t* d_pair_f2, orb_frame_bounds_t bounds, float nnratio,
-                                               int check_ori, int window, float* d_prev_xy, int32_t* d_matches12,
-                                               int32_t* d_nmatches, void* stream) {
+// The batched launch; `done` / `doneSeq`: a host call's completion flag (P == 1), else null.
+static int sfi_launch(const orb_keypoint_t* d_kps, const uint8_t* d_desc, const int32_t* d_counts, int cap, int P,
+                      const int32_t* d_pair_f1, const int32_t* d_pair_f2, orb_frame_bounds_t bounds, float nnratio,
+                      int check_ori, int window, float* d_prev_xy, int32_t* d_matches12, int32_t* d_nmatches,
+                      void* stream, int* done, int doneSeq) {
     if (!d_kps || !d_desc || !d_counts || cap <= 0 || P < 0 || !d_pair_f1 || !d_pair_f2 || !d_matches12 ||
         !d_nmatches)
         return set_err(ORB_EINVAL, "bad arguments");
@@ -4496,8 +4535,9 @@ int orb_search_for_initialization_batch_device(const orb_keypoint_t* d_kps, cons
     // any frame beyond (another producer, another scale factor) is redone exactly by
     // the large-capacity body in the same workgroup.  Fewer pairs than CUs: one work-group per CU anyway, and the
     // full capacity spares the per-frame path the fallback scratch.
-    const int nmax = P < 256 ? std::min(cap, 1024)
-                             : std::min({cap, 1024, std::max(MATCH_NMAX_MIN,
+    const int capA = (cap + 3) & ~3;  // nmax a multiple of 4: k_match_init's LDS arrays 16-B aligned
+    const int nmax = P < 256 ? std::min(capA, 1024)
+                             : std::min({capA, 1024, std::max(MATCH_NMAX_MIN,
                                                              (int)(((long long)cap * MATCH_NMAX_NUM / 40 + 31) & ~31))});
     const int nmaxBig = std::min(cap, MATCH_BIG_NMAX);
     // the large-capacity body runs in the same workgroup: the dynamic LDS covers both
@@ -4515,8 +4555,9 @@ int orb_search_for_initialization_batch_device(const orb_keypoint_t* d_kps, cons
     MatchGeom mg{bounds.min_x, bounds.max_x, bounds.min_y, bounds.max_y,
                  static_cast<float>(64) / static_cast<float>(bounds.max_x - bounds.min_x),
                  static_cast<float>(48) / static_cast<float>(bounds.max_y - bounds.min_y)};
-    MatchArgs A{d_kps, d_desc, d_counts, cap, nmax, d_pair_f1, d_pair_f2, mg, nnratio, check_ori, (float)window,
-                d_prev_xy, d_matches12, d_nmatches, P};
+    MatchArgs A{d_kps,      d_desc,    d_counts,     cap,       nmax,   d_pair_f1,         d_pair_f2,
+                mg,         nnratio,   check_ori,    (float)window, d_prev_xy, d_matches12, d_nmatches,
+                P,          P == 1 ? done : nullptr, doneSeq};
     hipStream_t st = (hipStream_t)stream;
     void* big = nullptr;
     std::unique_lock<std::mutex> lk(g_bigMu, std::defer_lock);
@@ -4530,6 +4571,15 @@ int orb_search_for_initialization_batch_device(const orb_keypoint_t* d_kps, cons
         hipLaunchKernelGGL(k_match_init<KM_THREADS>, dim3(P), dim3(KM_THREADS), lds, st, A, (uint8_t*)big, nmaxBig);
     HIP_TRY(hipGetLastError());
     return ORB_OK;
+}
+
+int orb_search_for_initialization_batch_device(const orb_keypoint_t* d_kps, const uint8_t* d_desc,
+                                               const int32_t* d_counts, int cap, int P, const int32_t* d_pair_f1,
+                                               const int32_t* d_pair_f2, orb_frame_bounds_t bounds, float nnratio,
+                                               int check_ori, int window, float* d_prev_xy, int32_t* d_matches12,
+                                               int32_t* d_nmatches, void* stream) {
+    return sfi_launch(d_kps, d_desc, d_counts, cap, P, d_pair_f1, d_pair_f2, bounds, nnratio, check_ori, window,
+                      d_prev_xy, d_matches12, d_nmatches, stream, nullptr, 0);
 }
 
 int orb_search_for_initialization(const orb_keypoint_t* kps1, const uint8_t* desc1, int n1, const orb_keypoint_t* kps2,
@@ -4555,7 +4605,8 @@ int orb_search_for_initialization(const orb_keypoint_t* kps1, const uint8_t* des
     if (!C) return set_err(ORB_EINVAL, "device ordinal out of range");
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     const size_t oK = 0, oD = oK + al((size_t)2 * cap * sizeof(orb_keypoint_t)), oC = oD + al((size_t)2 * cap * 32),
-                 oP = oC + al(6 * sizeof(int)), oM = oP + al((size_t)cap * 8), total = oM + al((size_t)cap * 4 + 4);
+                 oP = oC + al(6 * sizeof(int)), oM = oP + al((size_t)cap * 8), oF = oM + al((size_t)cap * 4 + 4),
+                 total = oF + 256;
     if (int r = C->reserve(0, total)) return r;
     uint8_t* hs = C->pinned;
     std::memcpy(hs + oK, kps1, (size_t)n1 * sizeof(orb_keypoint_t));
@@ -4568,10 +4619,29 @@ int orb_search_for_initialization(const orb_keypoint_t* kps1, const uint8_t* des
     hipStream_t s = C->stream;
     int* dc = (int*)(hs + oC);
     int* dm = (int*)(hs + oM);
-    int st = orb_search_for_initialization_batch_device((const orb_keypoint_t*)(hs + oK), hs + oD, dc, cap, 1, dc + 2,
-                                                        dc + 3, bounds, nnratio, check_ori, window, (float*)(hs + oP),
-                                                        dm, dm + cap, s);
-    const hipError_t e = hipStreamSynchronize(s);  // always drained: the staging is reused by the next call
+    // completion: the kernel's last act is a system-scope release then a flag store into the
+    // staging; the call spins on the flag (~1 us after the kernel's write, where a stream
+    // synchronisation takes several) and synchronises the stream only when the flag does not
+    // come (an error, or a kernel beyond the bound) -- the staging is then reused by the next call
+    // only after the flag: the kernel writes nothing after it
+    static thread_local int seq = 0;
+    seq = seq == 0x7fffffff ? 1 : seq + 1;
+    volatile int* flag = (volatile int*)(hs + oF);
+    *flag = 0;
+    int st = sfi_launch((const orb_keypoint_t*)(hs + oK), hs + oD, dc, cap, 1, dc + 2, dc + 3, bounds, nnratio, check_ori,
+                        window, (float*)(hs + oP), dm, dm + cap, s, (int*)(hs + oF), seq);
+    bool seen = false;
+    if (st == ORB_OK) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int spin = 0;; ++spin) {
+            if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) {
+                seen = true;
+                break;
+            }
+            if ((spin & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+        }
+    }
+    const hipError_t e = seen ? hipSuccess : hipStreamSynchronize(s);
     if (st) return st;
     if (e != hipSuccess) return set_err(ORB_EDEVICE, std::string("match: ") + hipGetErrorString(e));
     int nm = 0;

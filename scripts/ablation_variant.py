@@ -21,9 +21,9 @@ for a, b in zip(reps[0::2], reps[1::2]):
     if s.count(a) != 1:
         sys.exit(f"pattern occurs {s.count(a)} times: {a[:80]!r}")
     s = s.replace(a, b)
-src.write_text(s.replace('#include "../../include/orb_abi.h"', '#include "../include/orb_abi.h"'))
+src.write_text(s.replace('#include "../../include/', '#include "../include/'))
 for f in (tmp / "csrc").glob("*.hip"):
-    t = f.read_text().replace('"../../include/orb_abi.h"', '"../include/orb_abi.h"')
+    t = f.read_text().replace('"../../include/', '"../include/')
     f.write_text(t)
 units = [tmp / "csrc" / u for u in ("orb_hip.hip", "orb_match.hip", "orb_voc.hip", "orb_mappoint.hip",
                                     "orb_pipeline.hip", "orb_persist.hip", "orb_frame.hip", "orb_bow.hip")]

@@ -17,6 +17,8 @@
 #                        (scripts/stage_times.py at WL's shape), alternating twice
 #   abbench:WL:V1,..     quick:WL bench step of the in-tree library and each variant, alternating twice
 #   latency              the C++ per-call latency probe (build/latency_gpu)
+#   py:SCRIPT:ARGS       python scripts/SCRIPT ARGS (comma-separated), e.g. py:km_timing.py:build/variants/kmt.so,--per,2
+#   bin:NAME             a probe built on the CPU side, build/NAME
 set -o pipefail
 TAG=$1; shift
 OUT=gpurun_out/$TAG
@@ -97,8 +99,15 @@ PY
             done
         done ;;
     latency)
-        timeout -k 10 300 ./build/latency_gpu > "$OUT/latency.txt" 2>&1
+        timeout -k 10 300 ./build/latency_gpu 640 480 1000 200 > "$OUT/latency.txt" 2>&1
         rc=$?; tail -12 "$OUT/latency.txt" >> "$OUT/summary.txt"; fin latency $rc fatal ;;
+    py)  # py:SCRIPT:ARGS  python scripts/SCRIPT with comma-separated ARGS
+        f=$OUT/py_${a%.py}_${b//[^A-Za-z0-9]/_}.txt
+        timeout -k 10 300 python "scripts/$a" ${b//,/ } > "$f" 2>&1
+        rc=$?; grep -v amdgpu.ids "$f" | tail -4 | tee -a "$OUT/summary.txt"; fin "$S" $rc fatal ;;
+    bin)  # bin:NAME  build/NAME (a probe built on the CPU side)
+        timeout -k 10 300 "./build/$a" > "$OUT/bin_$a.txt" 2>&1
+        rc=$?; tail -12 "$OUT/bin_$a.txt" | tee -a "$OUT/summary.txt"; fin "$S" $rc fatal ;;
     *) note "unknown step $S"; exit 2 ;;
     esac
 done
