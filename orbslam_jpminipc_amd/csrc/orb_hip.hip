@@ -172,6 +172,12 @@ __constant__ uint32_t c_ic10[4 * 320];
 __constant__ uint32_t c_ic01[4 * 320];
 // k_orient_desc's row-pass B fragments: [N-tile t][lane l] = bytes j of B[16(l >> 4) + j][16t + (l & 15)]
 __constant__ uint4 c_rowB[4 * 64];  // 279 patch dwords per alignment, zero-padded to 5 x 64
+// OD_SB (the shared-blur variant): the column pass's A fragments (f16), [variant v][lane l] =
+// halves j of A[l & 15][k(l >> 4, j)]: out row o = l & 15 of a 16-row block, K slot (h, j) = the
+// row-pass sum of input row 4h + (j & 3) of an M-tile, its low (j < 4) or high (j >= 4) byte;
+// weight tap[d] (x 256 for the high byte), d = delta + 4h + (j & 3) - o, delta = the M-tile's
+// first row minus the block's (v 0: 0, v 1: 16, v 2: 12 without the tile's rows 0 .. 3)
+__constant__ uint4 c_colA[3 * 64];
 // ---- pyramid --------------------------------------------------------------------------
 // Level 0: copyMakeBorder(image, 16, BORDER_REFLECT_101); one thread per 16-byte chunk of a
 // padded row (pitch is a multiple of 16).  Interior chunks (source columns [x-16, x) inside the
@@ -1004,10 +1010,10 @@ __device__ __forceinline__ uint32_t compass8(uint32_t lf, uint32_t cc, uint32_t 
 typedef short s16x2_t __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ int fast_strength_packed(const uint8_t* p, int TP) {
-    const int off[16] = {3 * TP, 3 * TP + 1, 2 * TP + 2, TP + 3, 3, -TP + 3, -2 * TP + 2, -3 * TP + 1,
-                         -3 * TP, -3 * TP - 1, -2 * TP - 2, -TP - 3, -3, TP - 3, 2 * TP - 2, 3 * TP - 1};
     const uint32_t v = p[0];
 #if FS_I16
+    const int off[16] = {3 * TP, 3 * TP + 1, 2 * TP + 2, TP + 3, 3, -TP + 3, -2 * TP + 2, -3 * TP + 1,
+                         -3 * TP, -3 * TP - 1, -2 * TP - 2, -TP - 3, -3, TP - 3, 2 * TP - 2, 3 * TP - 1};
     s16x2_t d[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
@@ -2310,12 +2316,23 @@ __device__ __forceinline__ uint32_t blur_round(uint32_t T, bool tail) {
     return min((T + 0x7FFFu + bias) >> 16, 255u);
 }
 
+#ifndef OD_SB
+#define OD_SB 0  // 1: the shared-blur variant: both blur passes on the matrix cores
+#endif
+typedef _Float16 od_f16x8 __attribute__((ext_vector_type(8)));
+typedef float od_f32x4 __attribute__((ext_vector_type(4)));
+#define OD_SBP 14  // OD_SB: dwords per column of the blurred window (column-major; 14: conflict-free stores)
 #ifndef OD_WAVES
 #define OD_WAVES 4  // keypoint slots (waves) per workgroup (8 / 2 measured slower: 0.521 / 0.474 vs 0.468 ms c3;
                     // two slots per wave, lanes 0-31 / 32-63, 2 or 4 waves per workgroup: 0.531 / 0.567 vs
                     // 0.428 ms c3, 1.018 / 1.093 vs 0.818 c4 -- half the waves per CU, longer chains)
 #endif
-__global__ void __launch_bounds__(64 * OD_WAVES) k_orient_desc(const uint8_t* __restrict__ pyr, Geom g,
+#if OD_SB
+#define OD_ATTR __attribute__((amdgpu_waves_per_eu(8)))
+#else
+#define OD_ATTR
+#endif
+__global__ void __launch_bounds__(64 * OD_WAVES) OD_ATTR k_orient_desc(const uint8_t* __restrict__ pyr, Geom g,
                                                      const uint32_t* __restrict__ lvlOut,
                                                      const uint8_t* __restrict__ slotLvl,
                                                      const int2* __restrict__ lvlInfo, orb_keypoint_t* __restrict__ kps,
@@ -2364,6 +2381,11 @@ __global__ void __launch_bounds__(64 * OD_WAVES) k_orient_desc(const uint8_t* __
     // saved ~30 SALU per wave but let the loads sink below the window's, 0.420 -> 0.440 ms c3)
 #pragma unroll
     for (int t = 0; t < 4; ++t) Bf[t] = __builtin_bit_cast(i32x4v, c_rowB[t * 64 + lane]);
+#if OD_SB
+    od_f16x8 Ac[3];
+#pragma unroll
+    for (int v = 0; v < 3; ++v) Ac[v] = __builtin_bit_cast(od_f16x8, c_colA[v * 64 + lane]);
+#endif
     constexpr int NU = (2 * OD_WR + 1) * 4;  // 172 16-byte units
     uint4 v[3];
 #pragma unroll
@@ -2415,12 +2437,56 @@ __global__ void __launch_bounds__(64 * OD_WAVES) k_orient_desc(const uint8_t* __
     const int before = linfo.x, cntL = linfo.y;
     // an empty slot's wave does no work but stays for the workgroup's two barriers
     const bool active = k < g.kpCap && idx < cntL;  // wave-uniform
+#if OD_SB
+    const bool sbT = x + 18 < lg.xsimd_blur;  // no sample reaches the scalar tail: the shared blur
+    const int sbO0 = x - 5 - xa;
+#endif
     // IC_Angle's sums, then the angle arithmetic (fastAtan2, glibc sincosf: ~100 VALU, a fifth of a
     // keypoint's) once per workgroup: wave 0's lanes 0 .. 3 for the four slots, between the
     // two barriers, while the other waves run their row passes
     m01 = wave_total(m01);
     m10 = wave_total(m10);
+    typedef float f32x2v __attribute__((ext_vector_type(2)));
+    // The rBRIEF pattern: points 8 lane .. 8 lane + 7 (tests 4 lane .. 4 lane + 3), pair q =
+    // (x, y) of point 8 lane + q.  The rule of DESIGN §6.1, as code: eight fully coalesced
+    // dwordx2 rows of the pair-major table (each instruction reads 512 contiguous bytes, four
+    // cache lines no other pattern load touches; the float4 form read all 32 lines of the table
+    // with each of its four instructions, 64-B lane stride, and returned wrong data), issued by
+    // one asm statement and waited by another before the first sample (the registers are outputs
+    // of the first and in-out operands of the second: the compiler can neither move the loads nor
+    // read the registers early).  OD_PAT_EARLY 1: issued by the active waves once their own row
+    // pass is done, in flight across the second barrier; 2: before the first barrier (in flight
+    // across both, 16 more VGPRs live through the row pass); 0: after the second barrier.
+#ifndef OD_PAT_EARLY
+#define OD_PAT_EARLY 1
+#endif
+#ifndef OD_PAT_SPLIT
+#define OD_PAT_SPLIT 1  // 0: the wait inside the issuing asm (441 vs 427 us c3 for the float4 form)
+#endif
+    f32x2v pat[8];
+    auto issue_pattern = [&]() {
+        const uint32_t poff = 8u * (uint32_t)lane;
+        asm volatile(
+            "global_load_dwordx2 %0, %8, %9\n\t"
+            "global_load_dwordx2 %1, %8, %9 offset:512\n\t"
+            "global_load_dwordx2 %2, %8, %9 offset:1024\n\t"
+            "global_load_dwordx2 %3, %8, %9 offset:1536\n\t"
+            "global_load_dwordx2 %4, %8, %9 offset:2048\n\t"
+            "global_load_dwordx2 %5, %8, %9 offset:2560\n\t"
+            "global_load_dwordx2 %6, %8, %9 offset:3072\n\t"
+            "global_load_dwordx2 %7, %8, %9 offset:3584"
+#if !OD_PAT_SPLIT
+            "\n\ts_waitcnt vmcnt(0)"
+#endif
+            : "=&v"(pat[0]), "=&v"(pat[1]), "=&v"(pat[2]), "=&v"(pat[3]), "=&v"(pat[4]), "=&v"(pat[5]),
+              "=&v"(pat[6]), "=&v"(pat[7])
+            : "v"(poff), "s"((const float*)c_patternf)
+            : "memory");
+    };
     if (lane == 0) s_mom[wave] = make_int2(m01, m10);
+#if OD_PAT_EARLY == 2
+    if (active) issue_pattern();
+#endif
     lds_barrier();
     if (wave == 0 && lane < OD_WAVES) {
         const int2 mm = s_mom[lane];
@@ -2450,6 +2516,69 @@ __global__ void __launch_bounds__(64 * OD_WAVES) k_orient_desc(const uint8_t* __
         const uint32_t keep = h4 == 3 ? 0x000000FFu : 0xFFFFFFFFu;
         const uint32_t bias = h4 == 3 ? 0x0B7F7F00u : 0u;
         const i32x4v zero = {0, 0, 0, 0};
+#if OD_SB
+        // Shared blur: the row pass per N-tile t as below, then the column pass on the matrix cores
+        // too: D[o][n] = sum_k A[o][k] S[k][n] with S = the tile's row-pass sums split into bytes
+        // (each byte an f16 denormal b * 2^-24: its bits, no conversion) and A = the banded taps
+        // (x 256 for the high bytes, c_colA): D = T * 2^-24 exactly (f32, T < 2^24).  Out rows
+        // o = 0 .. 43 in blocks 0 / 16 / 28 (= the row pass's M-tiles; rows 28 .. 31 twice, rows
+        // 37 .. 43 partial and never read).  cvRound half-to-even of T / 65536 by the magic add,
+        // saturated, four rows per dword into the column-major blurred window (OD_SBP dwords per
+        // column).  Wave-uniform: keypoints whose samples reach the scalar tail take the sparse
+        // path below.
+        if (sbT) {
+            i32x4v a[3];
+#pragma unroll
+            for (int m = 0; m < 3; ++m) {
+                a[m].x = (int)A[m].x;
+                a[m].y = (int)A[m].y;
+                a[m].z = (int)A[m].z;
+                a[m].w = (int)((A[m].w & keep) | bias);
+            }
+            const od_f32x4 zf = {0.f, 0.f, 0.f, 0.f};
+            uint32_t* cb = (uint32_t*)W + r16 * OD_SBP + h4;
+            auto pack = [&](const i32x4v& c) {  // rows 4h .. 4h+3: low bytes, then high bytes
+                uint4 u;
+                u.x = __builtin_amdgcn_perm((uint32_t)c.y, (uint32_t)c.x, 0x0c040c00u);
+                u.y = __builtin_amdgcn_perm((uint32_t)c.w, (uint32_t)c.z, 0x0c040c00u);
+                u.z = __builtin_amdgcn_perm((uint32_t)c.y, (uint32_t)c.x, 0x0c050c01u);
+                u.w = __builtin_amdgcn_perm((uint32_t)c.w, (uint32_t)c.z, 0x0c050c01u);
+                return __builtin_bit_cast(od_f16x8, u);
+            };
+            auto emit = [&](const od_f32x4& D, uint32_t* dst) {
+                // (scalar fmas: this compiler folds a <2 x float> fma with splat constants into
+                // the low lane's result copied to both lanes, see the samples' magic add)
+                const uint32_t r0 = __builtin_bit_cast(uint32_t, __builtin_fmaf(D.x, 256.0f, 12582912.0f));
+                const uint32_t r1 = __builtin_bit_cast(uint32_t, __builtin_fmaf(D.y, 256.0f, 12582912.0f));
+                const uint32_t r2 = __builtin_bit_cast(uint32_t, __builtin_fmaf(D.z, 256.0f, 12582912.0f));
+                const uint32_t r3 = __builtin_bit_cast(uint32_t, __builtin_fmaf(D.w, 256.0f, 12582912.0f));
+                const uint32_t p01 = __builtin_amdgcn_perm(r1, r0, 0x05040100u);
+                const uint32_t p23 = __builtin_amdgcn_perm(r3, r2, 0x05040100u);
+                const u16x2 cap = {255, 255};
+                const uint32_t s01 = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, p01), cap));
+                const uint32_t s23 = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, p23), cap));
+                *dst = __builtin_amdgcn_perm(s23, s01, 0x06040200u);
+            };
+            const int nt = sbO0 <= 8 ? 3 : 4;  // N-tiles covering sum columns o0 .. o0 + 39
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                if (t == 3 && nt == 3) break;
+                const od_f16x8 S0 = pack(__builtin_amdgcn_mfma_i32_16x16x64_i8(a[0], Bf[t], zero, 0, 0, 0));
+                const od_f16x8 S1 = pack(__builtin_amdgcn_mfma_i32_16x16x64_i8(a[1], Bf[t], zero, 0, 0, 0));
+                od_f32x4 D0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(Ac[0], S0, zf, 0, 0, 0);
+                D0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(Ac[1], S1, D0, 0, 0, 0);
+                const od_f16x8 S2 = pack(__builtin_amdgcn_mfma_i32_16x16x64_i8(a[2], Bf[t], zero, 0, 0, 0));
+                od_f32x4 D1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(Ac[0], S1, zf, 0, 0, 0);
+                D1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(Ac[2], S2, D1, 0, 0, 0);
+                const od_f32x4 D2 = __builtin_amdgcn_mfma_f32_16x16x32_f16(Ac[0], S2, zf, 0, 0, 0);
+                uint32_t* ct = cb + 16 * t * OD_SBP;
+                emit(D0, ct);
+                emit(D1, ct + 4);
+                emit(D2, ct + 7);
+            }
+        } else
+#endif
+        {
         uint32_t* q3 = Hs + 2 * h4 * OD_HN + r16 + (r16 >= 8 ? 32 : 48);
 #pragma unroll
         for (int m = 0; m < 3; ++m) {
@@ -2473,44 +2602,9 @@ __global__ void __launch_bounds__(64 * OD_WAVES) k_orient_desc(const uint8_t* __
             }
             q3 += (kOdRow[m + (m < 2)] - kOdRow[m]) / 2 * OD_HN;
         }
+        }
     }
-    typedef float f32x2v __attribute__((ext_vector_type(2)));
-    // The rBRIEF pattern: points 8 lane .. 8 lane + 7 (tests 4 lane .. 4 lane + 3), pair q =
-    // (x, y) of point 8 lane + q.  The rule of DESIGN §6.1, as code: eight fully coalesced
-    // dwordx2 rows of the pair-major table (each instruction reads 512 contiguous bytes, four
-    // cache lines no other pattern load touches; the float4 form read all 32 lines of the table
-    // with each of its four instructions, 64-B lane stride, and returned wrong data), issued by
-    // one asm statement and waited by another before the first sample (the registers are outputs
-    // of the first and in-out operands of the second: the compiler can neither move the loads nor
-    // read the registers early).  OD_PAT_EARLY: issued by the active waves once their own row
-    // pass is done, in flight across the second barrier; else after it.
-#ifndef OD_PAT_EARLY
-#define OD_PAT_EARLY 1
-#endif
-#ifndef OD_PAT_SPLIT
-#define OD_PAT_SPLIT 1  // 0: the wait inside the issuing asm (441 vs 427 us c3 for the float4 form)
-#endif
-    f32x2v pat[8];
-    auto issue_pattern = [&]() {
-        const uint32_t poff = 8u * (uint32_t)lane;
-        asm volatile(
-            "global_load_dwordx2 %0, %8, %9\n\t"
-            "global_load_dwordx2 %1, %8, %9 offset:512\n\t"
-            "global_load_dwordx2 %2, %8, %9 offset:1024\n\t"
-            "global_load_dwordx2 %3, %8, %9 offset:1536\n\t"
-            "global_load_dwordx2 %4, %8, %9 offset:2048\n\t"
-            "global_load_dwordx2 %5, %8, %9 offset:2560\n\t"
-            "global_load_dwordx2 %6, %8, %9 offset:3072\n\t"
-            "global_load_dwordx2 %7, %8, %9 offset:3584"
-#if !OD_PAT_SPLIT
-            "\n\ts_waitcnt vmcnt(0)"
-#endif
-            : "=&v"(pat[0]), "=&v"(pat[1]), "=&v"(pat[2]), "=&v"(pat[3]), "=&v"(pat[4]), "=&v"(pat[5]),
-              "=&v"(pat[6]), "=&v"(pat[7])
-            : "v"(poff), "s"((const float*)c_patternf)
-            : "memory");
-    };
-#if OD_PAT_EARLY
+#if OD_PAT_EARLY == 1
     if (active) issue_pattern();
 #endif
     lds_barrier();  // s_trig is written (and the row-pass sums: LDS)
@@ -2581,6 +2675,29 @@ __global__ void __launch_bounds__(64 * OD_WAVES) k_orient_desc(const uint8_t* __
         vals[q] = (int)blur_round(T, decltype(tailC)::value && bx >= thr);
     }
     };
+#if OD_SB
+    if (sbT) {
+        // the blurred window's byte (column o0 + bits_x - kMagic, row bits_y - kMagic): one
+        // v_mad_u32_u24 of the low 24 bits of bits_x, the constants folded into the base
+        const uint32_t sbb = (uint32_t)(W - s_buf[0]) + (uint32_t)(4 * OD_SBP * o0) -
+                             (uint32_t)(4 * OD_SBP) * (kMagic & 0xFFFFFFu) - kMagic;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            f32x2v R;
+            asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,0] op_sel_hi:[1,1]\n\t"
+                "v_pk_fma_f32 %0, %1, %3, %0 op_sel:[0,0,0] op_sel_hi:[0,1,1]"
+                : "=&v"(R)
+                : "v"(pat[q]), "v"(rA), "v"(rB));
+            const uint32_t by = __builtin_bit_cast(uint32_t, R.x + 12582930.0f);
+            const uint32_t bx = __builtin_bit_cast(uint32_t, R.y + 12582930.0f);
+            bxs[q] = bx;
+            bys[q] = by;
+            uint32_t boff;
+            asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(boff) : "v"(bx), "v"(4u * OD_SBP), "v"(by + sbb));
+            vals[q] = s_buf[0][boff];
+        }
+    } else
+#endif
     if (tailAny)
         samples(std::true_type{});
     else
@@ -4205,6 +4322,26 @@ static int upload_pattern(int device) {
                     bf[(t * 64 + l) * 16 + j] = (uint8_t)v;
                 }
         HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_rowB), bf, sizeof(bf)));
+        // OD_SB column-pass fragments (f16 bit patterns)
+        uint16_t ca[3 * 64 * 8];
+        for (int v = 0; v < 3; ++v)
+            for (int l = 0; l < 64; ++l)
+                for (int j = 0; j < 8; ++j) {
+                    const int h = l >> 4, o = l & 15, ro = 4 * h + (j & 3);
+                    const int d = (v == 0 ? 0 : v == 1 ? 16 : 12) + ro - o;
+                    int wgt = (d >= 0 && d <= 6) ? tap[d] : 0;
+                    if (v == 2 && ro < 4) wgt = 0;  // rows 28 .. 31: the block's other tile holds them
+                    if (j >= 4) wgt *= 256;
+                    // a positive integer < 2^14 as f16: exponent e = floor(log2), 10-bit mantissa
+                    uint16_t hbits = 0;
+                    if (wgt) {
+                        int e = 0;
+                        while ((wgt >> (e + 1)) != 0) ++e;
+                        hbits = (uint16_t)(((e + 15) << 10) | (((wgt << 10) >> e) & 0x3FF));
+                    }
+                    ca[(v * 64 + l) * 8 + j] = hbits;
+                }
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(c_colA), ca, sizeof(ca)));
     }
     if (device >= 0 && device < 64) uploaded[device] = true;
     return ORB_OK;
