@@ -33,6 +33,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <climits>
 #include <cstring>
 #include <mutex>
@@ -52,6 +53,7 @@ constexpr int GRID_COLS = 64, GRID_ROWS = 48, NCELLS = GRID_COLS * GRID_ROWS;  /
 constexpr int TOPK = 8;
 constexpr int TH_HIGH = 100, TH_LOW = 50, HISTO = 30;  // ORBmatcher.cc:40-42
 constexpr int MAX_TARGET = 16384;                       // keypoints per target frame (LDS state)
+static_assert(NCELLS == 3 * 1024 && MAX_TARGET <= 65536, "k_grid_build: 3 cells per thread, u16 item indices");
 
 enum Mode : int {
     M_AREA_F = 0,   // Frame::GetFeaturesInArea
@@ -209,59 +211,66 @@ __device__ __forceinline__ void topk_insert(uint32_t (&t)[TOPK], uint32_t key) {
 __global__ void __launch_bounds__(1024) k_grid_build(const orb_keypoint_t* __restrict__ kps, int n, int minX,
                                                      int minY, float invW, float invH, int* __restrict__ cellStart,
                                                      int* __restrict__ items) {
+    // Counting sort in LDS: cell counts, their exclusive scan (wave prefix sums on DPP + the
+    // 16 wave totals: 3 barriers instead of round 5's 20-barrier tree), the keypoints placed by
+    // LDS cursors, each cell's few entries put back in index order in LDS, the list written out
+    // with one coalesced pass (round 5 sorted the cells in global memory: a dependent round trip
+    // per entry moved, 18-20 us per call).
     __shared__ int s_cnt[NCELLS];
-    __shared__ int s_part[1024];
-    const int tid = threadIdx.x;
+    __shared__ uint16_t s_items[MAX_TARGET];
+    __shared__ int s_wt[16];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    auto cell_of = [&](int i) {
+        const int px = (int)roundf((kps[i].x - (float)minX) * invW);
+        const int py = (int)roundf((kps[i].y - (float)minY) * invH);
+        return (px < 0 || px >= GRID_COLS || py < 0 || py >= GRID_ROWS) ? -1 : px * GRID_ROWS + py;
+    };
     for (int c = tid; c < NCELLS; c += 1024) s_cnt[c] = 0;
     __syncthreads();
     for (int i = tid; i < n; i += 1024) {
-        const int px = (int)roundf((kps[i].x - (float)minX) * invW);
-        const int py = (int)roundf((kps[i].y - (float)minY) * invH);
-        if (!(px < 0 || px >= GRID_COLS || py < 0 || py >= GRID_ROWS)) atomicAdd(&s_cnt[px * GRID_ROWS + py], 1);
+        const int c = cell_of(i);
+        if (c >= 0) atomicAdd(&s_cnt[c], 1);
     }
     __syncthreads();
-    // exclusive scan: 3 cells per thread
-    const int c0 = tid * 3;
+    const int c0 = tid * 3;  // 3 cells per thread (NCELLS = 3 x 1024)
     const int a = s_cnt[c0], b = s_cnt[c0 + 1], c = s_cnt[c0 + 2];
-    s_part[tid] = a + b + c;
+    const int incl = orbdev::wave_incl_scan(a + b + c);
+    if (lane == 63) s_wt[wave] = incl;
     __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {
-        const int v = tid >= o ? s_part[tid - o] : 0;
-        __syncthreads();
-        s_part[tid] += v;
-        __syncthreads();
-    }
-    const int base = s_part[tid] - (a + b + c);
+    int before = 0;
+    for (int w = 0; w < wave; ++w) before += s_wt[w];
+    const int base = before + incl - (a + b + c);
     cellStart[c0] = base;
     cellStart[c0 + 1] = base + a;
     cellStart[c0 + 2] = base + a + b;
-    if (tid == 1023) cellStart[NCELLS] = s_part[1023];
-    __syncthreads();
-    s_cnt[c0] = base;  // cursors
+    int total = 0;
+    for (int w = 0; w < 16; ++w) total += s_wt[w];
+    if (tid == 0) cellStart[NCELLS] = total;
+    s_cnt[c0] = base;  // cursors (each thread its own three cells)
     s_cnt[c0 + 1] = base + a;
     s_cnt[c0 + 2] = base + a + b;
     __syncthreads();
     for (int i = tid; i < n; i += 1024) {
-        const int px = (int)roundf((kps[i].x - (float)minX) * invW);
-        const int py = (int)roundf((kps[i].y - (float)minY) * invH);
-        if (!(px < 0 || px >= GRID_COLS || py < 0 || py >= GRID_ROWS))
-            items[atomicAdd(&s_cnt[px * GRID_ROWS + py], 1)] = i;
+        const int cc = cell_of(i);
+        if (cc >= 0) s_items[atomicAdd(&s_cnt[cc], 1)] = (uint16_t)i;
     }
-    __threadfence_block();
     __syncthreads();
-    // restore index order inside each cell (cells hold a handful of keypoints)
-    for (int cc = tid; cc < NCELLS; cc += 1024) {
-        const int s = cellStart[cc], e = s_cnt[cc];
-        for (int i = s + 1; i < e; ++i) {
-            const int v = items[i];
+    // index order inside each of this thread's cells (a handful of entries each)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int s0 = k == 0 ? base : k == 1 ? base + a : base + a + b, e = s_cnt[c0 + k];
+        for (int i = s0 + 1; i < e; ++i) {
+            const uint16_t v = s_items[i];
             int j = i - 1;
-            while (j >= s && items[j] > v) {
-                items[j + 1] = items[j];
+            while (j >= s0 && s_items[j] > v) {
+                s_items[j + 1] = s_items[j];
                 --j;
             }
-            items[j + 1] = v;
+            s_items[j + 1] = v;
         }
     }
+    __syncthreads();
+    for (int i = tid; i < total; i += 1024) items[i] = s_items[i];
 }
 
 // ---- k_query_prep ------------------------------------------------------------------------
@@ -602,14 +611,14 @@ __global__ void __launch_bounds__(256) k_area_fill(Job J) {
 // ---- k_resolve -------------------------------------------------------------------------
 constexpr int RES_CHUNK = 64;  // queries staged per chunk of the sequential pass
 // Exact rescan of query q against the live taken flags: the two smallest keys.
-__device__ void rescan_best2(const Job& J, int q, const QP& p, const uint8_t* s_taken, int lane, uint32_t* b1,
-                             uint32_t* b2) {
+template <class TAKEN>
+__device__ void rescan_best2_by(const Job& J, int q, const QP& p, TAKEN&& taken, int lane, uint32_t* b1, uint32_t* b2) {
     uint32_t d1[8];
     load_desc(J.qdesc + (size_t)qrow(J, q) * 8, d1);
     uint32_t lb = 0xFFFFFFFFu, ls = 0xFFFFFFFFu;
     const int m = J.mode;
     enum_candidates(J, p, lane, [&](int pos, int idx) {
-        if (s_taken[idx]) return;
+        if (taken(idx)) return;
         if (m == M_BOW_KFKF && !J.tflag[idx]) return;
         if (m == M_TRIANG && J.tflag[idx]) return;
         uint32_t d2[8];
@@ -628,6 +637,10 @@ __device__ void rescan_best2(const Job& J, int q, const QP& p, const uint8_t* s_
     const uint32_t g2 = wave_min(lb == g1 ? ls : lb);
     *b1 = g1;
     *b2 = g2;
+}
+__device__ void rescan_best2(const Job& J, int q, const QP& p, const uint8_t* s_taken, int lane, uint32_t* b1,
+                             uint32_t* b2) {
+    rescan_best2_by(J, q, p, [&](int idx) { return s_taken[idx] != 0; }, lane, b1, b2);
 }
 
 // SearchForTriangulation rescan: smallest untaken key with dist <= DistTh passing the
@@ -995,6 +1008,112 @@ __global__ void __launch_bounds__(256) k_resolve(Job J) {
     if (tid == 0) J.nOut[0] = s_nacc;
 }
 
+// SearchByProjection (local map, ORBmatcher.cc:49-125) without a sequential pass.  A query's
+// decision is a function of which of its candidates earlier queries took (`F.mvpMapPoints[idx]`
+// set earlier in the loop, ORBmatcher.cc:87-88): with takenBy[t] = the smallest query that
+// accepted target t (-1: taken before the call), query q sees t taken iff takenBy[t] < q.  Every
+// query is decided in parallel from the previous iteration's takenBy, the accepted targets give
+// the next takenBy (atomicMin), until takenBy repeats.  The sequential result is the unique
+// fixed point (query q depends only on queries < q, so by induction on q any fixed point equals
+// it) and the iteration reaches it: after iteration k queries 0 .. k-1 are final, and it stops
+// as soon as nothing changes (a handful of iterations: a decision changes only when an earlier
+// query's acceptance takes its best or second candidate).  A query whose top-8 holds too few
+// untaken entries is rescanned exactly (one wave, k_resolve's rescan with this predicate).
+// The loop is bounded by qn + 2 iterations (the induction's bound + the one that sees no
+// change); past it the kernel reports -1 matches and the call fails (cannot happen).
+#define RF_THREADS 1024
+size_t resolve_fix_lds(const Job& J) { return (size_t)2 * std::max(J.T.n, 1) * 4 + (size_t)std::max(J.qn, 1) * 4 + 16; }
+template <int MODE>
+__global__ void __launch_bounds__(RF_THREADS) k_resolve_fix(Job J) {
+    static_assert(MODE == M_LOCAL, "the fixed-point resolver covers SearchByProjection(local)");
+    extern __shared__ __attribute__((aligned(16))) int rsm[];
+    __shared__ int s_changed, s_nres, s_nacc;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int Tn = J.T.n;
+    int* s_tb = rsm;                  // takenBy, this iteration's input
+    int* s_tn = s_tb + max(Tn, 1);    // next iteration's
+    int* s_res = s_tn + max(Tn, 1);   // queries needing the exact rescan
+    for (int t = tid; t < Tn; t += RF_THREADS) s_tb[t] = J.taken0 && J.taken0[t] ? -1 : INT_MAX;
+    constexpr int need = needs_second(MODE) ? 2 : 1;
+    bool done = false;
+    for (int it = 0; it < J.qn + 2 && !done; ++it) {
+        for (int t = tid; t < Tn; t += RF_THREADS) s_tn[t] = J.taken0 && J.taken0[t] ? -1 : INT_MAX;
+        if (tid == 0) {
+            s_nres = 0;
+            s_changed = 0;
+        }
+        __syncthreads();
+        for (int q = tid; q < J.qn; q += RF_THREADS) {
+            if (!(J.qp[q].flags & 1)) continue;
+            const int cnt = J.cnt[q];
+            if (cnt == 0) continue;
+            const int k = min(cnt, TOPK);
+            uint32_t b1 = 0xFFFFFFFFu, b2 = 0xFFFFFFFFu, x1 = 0u, x2 = 0u;
+            int nUnt = 0;
+            for (int j = 0; j < k; ++j) {
+                const uint32_t x = J.topx[(size_t)q * TOPK + j];
+                if (s_tb[x & 0xFFFFFFu] < q) continue;
+                const uint32_t e = J.topk[(size_t)q * TOPK + j];
+                if (nUnt == 0) {
+                    b1 = e;
+                    x1 = x;
+                } else if (nUnt == 1) {
+                    b2 = e;
+                    x2 = x;
+                }
+                if (++nUnt == need) break;
+            }
+            if (cnt > TOPK && nUnt < need) {
+                s_res[atomicAdd(&s_nres, 1)] = q;
+                continue;
+            }
+            if (b1 == 0xFFFFFFFFu) continue;
+            const int bestDist2 = b2 != 0xFFFFFFFFu ? (int)(b2 >> 16) : INT_MAX;
+            const int bestLevel2 = b2 != 0xFFFFFFFFu ? (int)(x2 >> 24) : -1;
+            if (accept_rule<MODE>(J, (int)(b1 >> 16), bestDist2, (int)(x1 >> 24), bestLevel2))
+                atomicMin(&s_tn[x1 & 0xFFFFFFu], q);
+        }
+        __syncthreads();
+        for (int r = wave; r < s_nres; r += RF_THREADS / 64) {  // exact rescans, a wave each
+            const int q = s_res[r];
+            uint32_t b1, b2;
+            rescan_best2_by(J, q, J.qp[q], [&](int idx) { return s_tb[idx] < q; }, lane, &b1, &b2);
+            if (b1 == 0xFFFFFFFFu) continue;
+            const int i1 = key_idx(J, b1);
+            const int l1 = J.T.kps[i1].octave;
+            const int bestDist2 = b2 != 0xFFFFFFFFu ? (int)(b2 >> 16) : INT_MAX;
+            const int bestLevel2 = b2 != 0xFFFFFFFFu ? J.T.kps[key_idx(J, b2)].octave : -1;
+            if (lane == 0 && accept_rule<MODE>(J, (int)(b1 >> 16), bestDist2, l1, bestLevel2)) atomicMin(&s_tn[i1], q);
+        }
+        __syncthreads();
+        bool ch = false;
+        for (int t = tid; t < Tn; t += RF_THREADS) {
+            ch |= s_tn[t] != s_tb[t];
+            s_tb[t] = s_tn[t];
+        }
+        if (ch) s_changed = 1;
+        __syncthreads();
+        done = s_changed == 0;
+        __syncthreads();  // s_changed read by all before the next iteration resets it
+    }
+    if (tid == 0) s_nacc = 0;
+    __syncthreads();
+    int acc = 0;
+    for (int t = tid; t < J.outN; t += RF_THREADS) {  // outN == Tn (by target)
+        const int v = s_tb[t];
+        const bool a = v >= 0 && v != INT_MAX;
+        J.out[t] = a ? v : -1;
+        acc += a;
+    }
+    acc = wave_sum(acc);
+    if (lane == 0 && acc) atomicAdd(&s_nacc, acc);
+    __syncthreads();
+    if (tid == 0) {
+        J.nOut[0] = done ? s_nacc : -1;
+        J.nOut[1] = 0;  // (iterations: debug builds)
+    }
+}
+
 // SearchBySim3 agreement (ORBmatcher.cc:1489-1502): match12[i1] = idx2 iff vnMatch2[idx2] == i1.
 __global__ void k_sim3_agree(const int* __restrict__ m1, int n1, const int* __restrict__ m2, int* __restrict__ out,
                              int* __restrict__ nOut) {
@@ -1089,6 +1208,35 @@ OrbHostCtx* orb_internal_thread_ctx(int device) {
 
 namespace {
 // Bump allocator over one device buffer; `stage` copies a host array into it.
+// The staged inputs of a call, copied into the arena by a kernel reading the pinned staging
+// (mapped host memory) directly: in-stream with the call's kernels, so no copy-engine hand-off
+// (the SDMA copy of ~100 KB took 8.5 us plus ~8 us until the first kernel started, rocprofv3
+// timeline of build/latency_gpu, profiles/r06/).  16-B units, a grid-stride loop.
+__global__ void __launch_bounds__(256) k_stage_copy(uint4* __restrict__ dst, const uint4* __restrict__ src, size_t n16,
+                                                    const uint8_t* __restrict__ srcb, uint8_t* __restrict__ dstb,
+                                                    int tail) {
+    const size_t stride = (size_t)gridDim.x * 256;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n16; i += stride) dst[i] = src[i];
+    if (blockIdx.x == 0 && (int)threadIdx.x < tail) dstb[threadIdx.x] = srcb[threadIdx.x];
+}
+#define STAGE_KERNEL_MAX (8u << 20)  // larger uploads take the copy engine
+// The results of a call, copied from the arena into the pinned staging by one workgroup that
+// then publishes a completion flag (system-scope release, as k_match_init's host call): the
+// host spins on the flag instead of a D2H copy command plus a stream synchronisation.
+__global__ void __launch_bounds__(256) k_stage_out(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
+                                                   int bytes, int* __restrict__ flag, int seq) {
+    const int n16 = bytes >> 4;
+    for (int i = threadIdx.x; i < n16; i += 256) ((uint4*)dst)[i] = ((const uint4*)src)[i];
+    if ((int)threadIdx.x < (bytes & 15)) dst[(n16 << 4) + threadIdx.x] = src[(n16 << 4) + threadIdx.x];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+#define STAGE_OUT_MAX (256u << 10)  // larger results take a D2H copy + stream synchronisation
+
 struct Arena {
     std::vector<std::pair<size_t, std::pair<const void*, size_t>>> uploads;
     size_t size = 0;
@@ -1144,8 +1292,10 @@ struct Call {
     // allocate (grow) the arena and upload every staged array in one H2D copy
     std::vector<std::pair<void*, std::pair<size_t, size_t>>> pending;  // (host, (off, bytes)) downloads
     bool inflight = false;  // work queued on ctx->stream since the last sync()
+    size_t flagOff = 0;  // the completion flag's offset in the staging (past the arena's)
     int commit() {
-        if (int st = ctx->reserve(A.size, A.size)) return st;
+        flagOff = (A.size + 255) & ~(size_t)255;
+        if (int st = ctx->reserve(A.size, flagOff + 256)) return st;
         inflight = true;
         base = ctx->buf;
         size_t hi = 0;
@@ -1153,21 +1303,58 @@ struct Call {
             std::memcpy(ctx->pinned + u.first, u.second.first, u.second.second);
             hi = std::max(hi, u.first + u.second.second);
         }
-        if (hi) HIPCHK(hipMemcpyAsync(base, ctx->pinned, hi, hipMemcpyHostToDevice, ctx->stream));
-        return ORB_OK;
-    }
-    // D2H through the pinned staging (the arena offset is also the staging offset); the
-    // caller's buffer is filled by sync()
-    int download(void* host, size_t off, size_t bytes) {
-        inflight = true;
-        if (bytes) {
-            HIPCHK(hipMemcpyAsync(ctx->pinned + off, base + off, bytes, hipMemcpyDeviceToHost, ctx->stream));
-            pending.push_back({host, {off, bytes}});
+        if (hi && hi <= STAGE_KERNEL_MAX) {
+            const size_t n16 = hi >> 4;
+            const int tail = (int)(hi & 15);
+            const unsigned grid = (unsigned)std::min<size_t>(64, std::max<size_t>(1, (n16 + 255) / 256));
+            hipLaunchKernelGGL(k_stage_copy, dim3(grid), dim3(256), 0, ctx->stream, (uint4*)base,
+                               (const uint4*)ctx->pinned, n16, ctx->pinned + (n16 << 4), base + (n16 << 4), tail);
+            HIPCHK(hipGetLastError());
+        } else if (hi) {
+            HIPCHK(hipMemcpyAsync(base, ctx->pinned, hi, hipMemcpyHostToDevice, ctx->stream));
         }
         return ORB_OK;
     }
+    // D2H through the pinned staging (the arena offset is also the staging offset): download()
+    // records a region, sync() copies the span of all recorded regions in ONE D2H copy (results
+    // are taken last and lie together: a copy costs ~5 us of latency, the bytes between them
+    // nothing) and then fills the callers' buffers
+    int download(void* host, size_t off, size_t bytes) {
+        inflight = true;
+        if (bytes) pending.push_back({host, {off, bytes}});
+        return ORB_OK;
+    }
     int sync() {
-        HIPCHK(hipStreamSynchronize(ctx->stream));
+        bool seen = false;
+        if (!pending.empty()) {
+            size_t lo = pending[0].second.first, hi = lo;
+            for (auto& d : pending) {
+                lo = std::min(lo, d.second.first);
+                hi = std::max(hi, d.second.first + d.second.second);
+            }
+            if (hi - lo <= STAGE_OUT_MAX) {
+                static thread_local int seq = 0;
+                seq = seq == 0x7fffffff ? 1 : seq + 1;
+                volatile int* flag = (volatile int*)(ctx->pinned + flagOff);
+                *flag = 0;
+                hipLaunchKernelGGL(k_stage_out, dim3(1), dim3(256), 0, ctx->stream, ctx->pinned + lo, base + lo,
+                                   (int)(hi - lo), (int*)(ctx->pinned + flagOff), seq);
+                HIPCHK(hipGetLastError());
+                const auto t0 = std::chrono::steady_clock::now();
+                for (int spin = 0;; ++spin) {
+                    if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) {
+                        seen = true;
+                        break;
+                    }
+                    if ((spin & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+                }
+            } else {
+                HIPCHK(hipMemcpyAsync(ctx->pinned + lo, base + lo, hi - lo, hipMemcpyDeviceToHost, ctx->stream));
+            }
+        }
+        // (the flag is the kernel's last write, nothing of the call runs after it; without it --
+        // no results, an error, a call past the bound -- the stream is synchronised)
+        if (!seen) HIPCHK(hipStreamSynchronize(ctx->stream));
         inflight = false;
         for (auto& d : pending) std::memcpy(d.first, ctx->pinned + d.second.first, d.second.second);
         pending.clear();
@@ -1303,6 +1490,17 @@ int run_job(const Call& C, const Job& J) {
 #undef SET_RESOLVE_LDS
         attr_set[C.device] = true;
     }
+    if (J.mode == M_LOCAL && resolve_fix_lds(J) <= 150 * 1024) {
+        static std::atomic<bool> fix_attr[64] = {};
+        if (!fix_attr[C.device].load()) {
+            HIPCHK(hipFuncSetAttribute((const void*)k_resolve_fix<M_LOCAL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       150 * 1024));
+            fix_attr[C.device] = true;
+        }
+        hipLaunchKernelGGL(k_resolve_fix<M_LOCAL>, dim3(1), dim3(RF_THREADS), resolve_fix_lds(J), s, J);
+        HIPCHK(hipGetLastError());
+        return ORB_OK;
+    }
     switch (J.mode) {
 #define LAUNCH_RESOLVE(M) \
     case M: hipLaunchKernelGGL(k_resolve<M>, dim3(1), dim3(256), lds, s, J); break;
@@ -1405,8 +1603,7 @@ int bow_match_nodes(int mode, const orb_frame_view_t* V1, const uint8_t* flag1, 
                                         C.at<int32_t>(oM), C.at<int32_t>(oM) + cap, C.ctx->stream);
     if (st) return st;
     int nm = 0;
-    if ((st = C.download(out, oM, (size_t)outN * 4)) || (st = C.download(&nm, oM + (size_t)cap * 4, 4)) ||
-        (st = C.sync()))
+    if ((st = C.download(out, oM, (size_t)outN * 4)) || (st = C.download(&nm, oM + (size_t)cap * 4, 4)) || (st = C.sync()))
         return st;
     *n_out = nm;
     return ORB_OK;
@@ -1549,6 +1746,7 @@ int grid_match(Job J, const orb_frame_view_t* T, const uint8_t* taken, const Gri
     int nm = 0;
     if ((st = C.download(out, jo.out, (size_t)outN * 4)) || (st = C.download(&nm, jo.nOut, 4)) || (st = C.sync()))
         return st;
+    if (nm < 0) return fail(ORB_EDEVICE, "local-map resolver did not converge");
     *n_out = nm;
     return ORB_OK;
 }

@@ -17,6 +17,7 @@
 #                        (scripts/stage_times.py at WL's shape), alternating twice
 #   abbench:WL:V1,..     quick:WL bench step of the in-tree library and each variant, alternating twice
 #   latency              the C++ per-call latency probe (build/latency_gpu)
+#   latprof              the same probe under rocprofv3 --kernel-trace --memory-copy-trace
 #   py:SCRIPT:ARGS       python scripts/SCRIPT ARGS (comma-separated), e.g. py:km_timing.py:build/variants/kmt.so,--per,2
 #   bin:NAME             a probe built on the CPU side, build/NAME
 set -o pipefail
@@ -101,6 +102,10 @@ PY
     latency)
         timeout -k 10 300 ./build/latency_gpu 640 480 1000 200 > "$OUT/latency.txt" 2>&1
         rc=$?; tail -12 "$OUT/latency.txt" >> "$OUT/summary.txt"; fin latency $rc fatal ;;
+    latprof)  # the latency probe under rocprofv3 (kernels + copies): per-call device timelines
+        timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/latprof" -o run --output-format csv -- \
+            ./build/latency_gpu 640 480 1000 50 > "$OUT/latprof.log" 2>&1
+        rc=$?; fin latprof $rc fatal ;;
     py)  # py:SCRIPT:ARGS  python scripts/SCRIPT with comma-separated ARGS
         f=$OUT/py_${a%.py}_${b//[^A-Za-z0-9]/_}.txt
         timeout -k 10 300 python "scripts/$a" ${b//,/ } > "$f" 2>&1
