@@ -2786,6 +2786,9 @@ struct MatchGeom {
 #endif
 #define KM_WIDE_PAIRS 256  // fewer pairs: 16-wave workgroups (phase 1: NT / 256 lanes per query)
 #define MATCH_BIG_NMAX 8192
+#ifndef KM_FIX
+#define KM_FIX 1  // 0: the sequential (speculated) phase 2 for every launch
+#endif
 #ifndef KM_TIMING  // 1: per-phase s_memrealtime sums of k_match_init's pairs (experiment builds only)
 #define KM_TIMING 0
 #endif
@@ -2821,6 +2824,7 @@ struct MatchArgs {
     int P;
     int* done;    // host call (P == 1): pinned flag the kernel sets to doneSeq once its outputs are
     int doneSeq;  // visible to the host (the caller spins on it instead of a stream synchronisation)
+    int fixOff;   // LDS byte offset of the fixed-point phase 2's arrays (16-wave launches), 0: sequential
 };
 
 // ORBmatcher.cc:664-670: the rotation's histogram bin (HISTO_LENGTH 30, factor 1/30)
@@ -2913,7 +2917,41 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
     for (int i = tid; i < n1; i += NT) s_m12[i] = K1[i].octave == 0;  // level1 > 0 -> continue (ORBmatcher.cc:615)
     if constexpr (BIG) __threadfence_block();
     __syncthreads();
-    if (wave == 0) {  // in-place, in-order compaction (one wave: reads precede writes)
+    if constexpr (!BIG && NT == 1024) {
+        // 16 waves: both lists compacted by the whole workgroup, 1024 entries per round (per wave
+        // a ballot count, the waves' offsets from a 16-entry table); the single-wave loops
+        // below took ~2.6 us per pair alone
+        __shared__ int s_wc2[16], s_wc1[16];
+        int base2 = 0, base1 = 0;
+        for (int i0 = 0; i0 < max(n1, n2); i0 += NT) {
+            const int i = i0 + tid;
+            const uint32_t key = i < n2 ? s_key[i] : 0xFFFFFFFFu;
+            const bool ok2 = key != 0xFFFFFFFFu;
+            const bool ok1 = i < n1 && s_m12[i];
+            const uint64_t m2 = __ballot(ok2), m1 = __ballot(ok1);
+            if (lane == 0) {
+                s_wc2[wave] = __popcll(m2);
+                s_wc1[wave] = __popcll(m1);
+            }
+            __syncthreads();  // (also: every read of s_key's round precedes the writes below)
+            int o2 = base2, o1 = base1, t2 = 0, t1 = 0;
+            for (int w = 0; w < 16; ++w) {
+                const int c2 = s_wc2[w], c1 = s_wc1[w];
+                if (w < wave) o2 += c2, o1 += c1;
+                t2 += c2;
+                t1 += c1;
+            }
+            if (ok2) s_key[o2 + lanes_below(m2)] = key;
+            if (ok1 && o1 + lanes_below(m1) < nmax) s_q2i[o1 + lanes_below(m1)] = i;
+            base2 += t2;
+            base1 += t1;
+            __syncthreads();
+        }
+        if (tid == 0) {
+            s_n2c = base2;
+            s_n1c = base1;
+        }
+    } else if (wave == 0) {  // in-place, in-order compaction (one wave: reads precede writes)
         int base = 0;
         for (int i0 = 0; i0 < n2; i0 += 64) {
             const uint32_t key = i0 + lane < n2 ? s_key[i0 + lane] : 0xFFFFFFFFu;
@@ -2942,11 +2980,21 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
         return true;
     }
     KM_T(1);
-    // rank F2 candidates by traversal key -> slot
-    for (int t = tid; t < n2c; t += NT) {
+    // rank F2 candidates by traversal key -> slot.  16-wave launches with few candidates: LPK
+    // adjacent lanes per key, each counting every LPK-th key, summed on DPP (one thread per key
+    // counted all n2c keys: ~3.5 us per pair alone at 217 candidates)
+    int lpk = 1;
+    if constexpr (!BIG && NT == 1024) lpk = n2c <= 256 ? 4 : n2c <= 512 ? 2 : 1;
+    for (int t0 = tid; t0 < n2c * lpk; t0 += NT) {
+        const int t = t0 / lpk, sub = t0 - t * lpk;  // (lpk divides NT: a key's lanes share a wave)
         const uint32_t k = s_key[t];
         int rank = 0;
-        for (int u = 0; u < n2c; ++u) rank += s_key[u] < k;
+        for (int u = sub; u < n2c; u += lpk) rank += s_key[u] < k;
+        if constexpr (!BIG && NT == 1024) {
+            if (lpk >= 2) rank += __builtin_amdgcn_mov_dpp(rank, 0xB1, 0xF, 0xF, false);  // quad_perm xor 1
+            if (lpk >= 4) rank += __builtin_amdgcn_mov_dpp(rank, 0x4E, 0xF, 0xF, false);  // quad_perm xor 2
+        }
+        if (sub != 0) continue;
         const int i2 = (int)(k & 0xFFFF);
         const orb_keypoint_t kp = K2[i2];
         s_x2[rank] = kp.x;
@@ -3074,7 +3122,9 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
     // a batch runs alone on the whole wave.
     // the exact rescan of query q0's whole window, on all 64 lanes of wave 0 (a query whose
     // truncated top-8 holds fewer than two live candidates)
-    auto rescan_query = [&](const int q0) {
+    // the exact rescan of query q0's whole window on all 64 lanes of a wave: the smallest live
+    // key and the second-smallest live distance (live(j, dist): candidate slot j not excluded)
+    auto rescan_best = [&](const int q0, auto&& live, uint32_t& gbOut, int& contribOut) {
         const int i1 = s_q2i[q0];
         const float qx = s_qx[q0], qy = s_qy[q0];
         const int minCX = max(0, (int)floorf((qx - mg.minX - r) * mg.invW));
@@ -3096,7 +3146,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
             if (cx < minCX || cx > maxCX || cy < minCY || cy > maxCY) continue;
             if (fabsf(s_x2[j] - qx) > r || fabsf(s_y2[j] - qy) > r) continue;
             const int dist = hamming256(d1, s_d2 + j * 8);
-            if ((int)(s_st[j].x & 0xFFFFu) <= dist) continue;
+            if (!live(j, dist)) continue;
             const uint32_t key = ((uint32_t)dist << KB) | (uint32_t)j;
             if (key < lb) {
                 if (lb != 0xFFFFFFFFu) ls = (int)(lb >> KB);
@@ -3109,7 +3159,15 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
         gb = wave_min_u32(gb);
         int contrib = (lb == gb) ? ls : (lb == 0xFFFFFFFFu ? 0x7fffffff : (int)(lb >> KB));
         contrib = (int)wave_min_u32((uint32_t)contrib);  // (non-negative)
+        gbOut = gb;
+        contribOut = contrib;
+    };
+    auto rescan_query = [&](const int q0) {
+        uint32_t gb;
+        int contrib;
+        rescan_best(q0, [&](int j, int dist) { return (int)(s_st[j].x & 0xFFFFu) > dist; }, gb, contrib);
         if (gb == 0xFFFFFFFFu) return;
+        const int i1 = s_q2i[q0];
         const int rDist = (int)(gb >> KB), rSlot = (int)(gb & SLOT);
         if (rDist <= 50 && (float)rDist < (float)contrib * nnratio && lane == 0) {
             const uint2 sb = s_st[rSlot];
@@ -3120,7 +3178,144 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
             s_bslot[i1] = (short)rSlot;
         }
     };
-    if (wave == 0 && n1c > 0) {
+    // Phase 2 as a fixed point (the single-pair call, 16 waves, when its arrays fit the LDS):
+    // query q's decision depends only on the earlier queries' acceptances -- candidate slot s is
+    // live for q iff dist < MD_q(s) = min{d_j : j < q accepted s} (vMatchedDistance as q sees
+    // it) -- so every query is decided in parallel from the previous iteration's acceptances
+    // until they repeat; the sequential result is the unique fixed point and is reached (after
+    // iteration k the first k queries are final; SearchByProjection(local)'s resolver, orb_match).
+    // Up to three acceptors per slot and iteration (more: the sequential pass below decides).
+    // Final: every accepting query keeps its slot (bins count the stolen ones too), the slot's
+    // last acceptor owns the match (vnMatches21).
+    bool fixDone = false;
+    if constexpr (!BIG && NT == 1024) {
+        if (A.fixOff) {
+            __shared__ int s_fn, s_fch, s_fovf;
+            uint32_t* faB[2];
+            int* fcB[2];
+            faB[0] = (uint32_t*)(smem + A.fixOff);
+            faB[1] = faB[0] + 3 * nmax;
+            fcB[0] = (int*)(faB[1] + 3 * nmax);
+            fcB[1] = fcB[0] + nmax;
+            int* fdec = fcB[1] + nmax;  // per query: (dist << 16) | slot, -1 none
+            int* fnew = fdec + nmax;
+            uint16_t* fres = (uint16_t*)(fnew + nmax);
+            for (int i = tid; i < n2c; i += NT) fcB[0][i] = 0;
+            for (int i = tid; i < n1c; i += NT) fdec[i] = -1;
+            if (tid == 0) s_fovf = 0;
+            const int q = tid;
+            const bool qin = q < n1c;
+            const int cnt = qin ? s_lcnt[q] : 0;
+            uint32_t el[MATCH_TOPK];
+#pragma unroll
+            for (int k = 0; k < MATCH_TOPK; ++k) el[k] = qin ? s_list[q * MATCH_TOPK + k] : 0xFFFFFFFFu;
+            int cur = 0;
+            bool conv = false;
+            for (int it = 0; it < n1c + 2 && !conv; ++it) {
+                const uint32_t* fa = faB[cur];
+                const int* fc = fcB[cur];
+                uint32_t* na = faB[cur ^ 1];
+                int* nc = fcB[cur ^ 1];
+                for (int i = tid; i < n2c; i += NT) nc[i] = 0;
+                if (tid == 0) {
+                    s_fn = 0;
+                    s_fch = 0;
+                }
+                __syncthreads();
+                auto md = [&](int sl, int qq) {  // MD_qq(sl): 0xFFFF = INT_MAX
+                    int m = 0xFFFF;
+                    const int c = min(fc[sl], 3);
+                    for (int i = 0; i < c; ++i) {
+                        const uint32_t v = fa[3 * sl + i];
+                        if ((int)(v >> 9) < qq) m = min(m, (int)(v & 511u));
+                    }
+                    return m;
+                };
+                int dec = -1;
+                if (qin && cnt > 0) {
+                    const int k = min(cnt, MATCH_TOPK);
+                    uint32_t b1 = 0xFFFFFFFFu, b2 = 0xFFFFFFFFu;
+#pragma unroll
+                    for (int j = 0; j < MATCH_TOPK; ++j) {
+                        if (j < k && b2 == 0xFFFFFFFFu) {
+                            const uint32_t e = el[j];
+                            if (md((int)(e & SLOT), q) > (int)(e >> KB)) {
+                                if (b1 == 0xFFFFFFFFu)
+                                    b1 = e;
+                                else
+                                    b2 = e;
+                            }
+                        }
+                    }
+                    if (cnt > MATCH_TOPK && b2 == 0xFFFFFFFFu) {
+                        fres[atomicAdd(&s_fn, 1)] = (uint16_t)q;
+                        dec = -2;
+                    } else if (b1 != 0xFFFFFFFFu) {
+                        const int bd = (int)(b1 >> KB);
+                        const int second = b2 != 0xFFFFFFFFu ? (int)(b2 >> KB) : 0x7fffffff;
+                        if (bd <= 50 && (float)bd < (float)second * nnratio) dec = (bd << 16) | (int)(b1 & SLOT);
+                    }
+                    if (dec >= 0) {
+                        const int sl = dec & 0xFFFF;
+                        const int ix = atomicAdd(&nc[sl], 1);
+                        if (ix < 3)
+                            na[3 * sl + ix] = ((uint32_t)q << 9) | (uint32_t)(dec >> 16);
+                        else
+                            s_fovf = 1;
+                    }
+                }
+                if (qin && dec != -2) fnew[q] = dec;
+                __syncthreads();
+                const int nres = s_fn;
+                for (int rr = wave; rr < nres; rr += NT / 64) {  // exact rescans, a wave each
+                    const int qq = fres[rr];
+                    uint32_t gb;
+                    int contrib;
+                    rescan_best(qq, [&](int j, int dist) { return md(j, qq) > dist; }, gb, contrib);
+                    int d2 = -1;
+                    if (gb != 0xFFFFFFFFu) {
+                        const int rd = (int)(gb >> KB);
+                        if (rd <= 50 && (float)rd < (float)contrib * nnratio) d2 = (rd << 16) | (int)(gb & SLOT);
+                    }
+                    if (lane == 0) {
+                        fnew[qq] = d2;
+                        if (d2 >= 0) {
+                            const int sl = d2 & 0xFFFF;
+                            const int ix = atomicAdd(&nc[sl], 1);
+                            if (ix < 3)
+                                na[3 * sl + ix] = ((uint32_t)qq << 9) | (uint32_t)(d2 >> 16);
+                            else
+                                s_fovf = 1;
+                        }
+                    }
+                }
+                __syncthreads();
+                if (qin && fnew[q] != fdec[q]) {
+                    fdec[q] = fnew[q];
+                    s_fch = 1;
+                }
+                __syncthreads();
+                conv = s_fch == 0 || s_fovf != 0;
+                cur ^= 1;
+                __syncthreads();  // s_fch / s_fovf read by every thread before the next reset
+            }
+            if (conv && s_fovf == 0) {
+                fixDone = true;
+                // (the lists of the last iteration, faB[cur] / fcB[cur], hold the final acceptances)
+                const uint32_t* fa = faB[cur];
+                const int* fc = fcB[cur];
+                if (qin && fdec[q] >= 0) s_bslot[s_q2i[q]] = (short)(fdec[q] & 0xFFFF);
+                for (int sl = tid; sl < n2c; sl += NT) {
+                    const int c = min(fc[sl], 3);
+                    int owner = -1;
+                    for (int i = 0; i < c; ++i) owner = max(owner, (int)(fa[3 * sl + i] >> 9));
+                    if (owner >= 0) s_m12[s_q2i[owner]] = (int)(s_st[sl].y & 0x1FFFu);
+                }
+            }
+            __syncthreads();
+        }
+    }
+    if (!fixDone && wave == 0 && n1c > 0) {
         const int grp = lane >> 3, cand = lane & 7;
         int q0 = 0;
         while (q0 < n1c) {
@@ -4678,9 +4873,18 @@ static int sfi_launch(const orb_keypoint_t* d_kps, const uint8_t* d_desc, const 
                                                              (int)(((long long)cap * MATCH_NMAX_NUM / 40 + 31) & ~31))});
     const int nmaxBig = std::min(cap, MATCH_BIG_NMAX);
     // the large-capacity body runs in the same workgroup: the dynamic LDS covers both
-    const size_t lds = std::max(match_lds_bytes(cap, nmax), cap > nmax ? match_big_lds_bytes(cap, nmaxBig) : 0);
+    size_t lds = std::max(match_lds_bytes(cap, nmax), cap > nmax ? match_big_lds_bytes(cap, nmaxBig) : 0);
     if (lds > 159 * 1024)  // 160 KB per CU minus the kernel's static LDS
         return set_err(ORB_ENOTSUP, "per-frame keypoint capacity too large for LDS");
+    // the fixed-point phase 2 of the 16-wave launch: two acceptor lists (3 entries + count per
+    // slot), decisions old / new and the rescan list per query, after the body's arrays
+    int fixOff = 0;
+    const size_t fixAt = (match_lds_bytes(cap, nmax) + 15) & ~(size_t)15;
+    const size_t fixEnd = fixAt + (size_t)nmax * (2 * 16 + 8 + 2);
+    if (P < KM_WIDE_PAIRS && KM_FIX && fixEnd <= 158 * 1024) {
+        fixOff = (int)fixAt;
+        lds = std::max(lds, fixEnd);
+    }
     static std::once_flag attrOnce;
     std::call_once(attrOnce, [] {
         (void)hipFuncSetAttribute((const void*)k_match_init<KM_THREADS>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -4694,7 +4898,7 @@ static int sfi_launch(const orb_keypoint_t* d_kps, const uint8_t* d_desc, const 
                  static_cast<float>(48) / static_cast<float>(bounds.max_y - bounds.min_y)};
     MatchArgs A{d_kps,      d_desc,    d_counts,     cap,       nmax,   d_pair_f1,         d_pair_f2,
                 mg,         nnratio,   check_ori,    (float)window, d_prev_xy, d_matches12, d_nmatches,
-                P,          P == 1 ? done : nullptr, doneSeq};
+                P,          P == 1 ? done : nullptr, doneSeq, fixOff};
     hipStream_t st = (hipStream_t)stream;
     void* big = nullptr;
     std::unique_lock<std::mutex> lk(g_bigMu, std::defer_lock);
