@@ -2798,13 +2798,17 @@ __device__ unsigned long long g_kmtime[8];
 #else
 #define KM_T(i)
 #endif
+// Insert key into the sorted list t, keeping the smallest entries: the new t[i] is the median
+// of (old t[i-1], key, old t[i]) -- one v_med3_u32 per entry, all independent (the min / max
+// insertion chain was two dependent ops per entry)
 __device__ __forceinline__ void topk_insert(uint32_t (&t)[MATCH_TOPK], uint32_t key) {
 #pragma unroll
-    for (int i = 0; i < MATCH_TOPK; ++i) {
-        uint32_t lo = min(t[i], key), hi = max(t[i], key);
-        t[i] = lo;
-        key = hi;
+    for (int i = MATCH_TOPK - 1; i >= 1; --i) {
+        uint32_t r;
+        asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(t[i - 1]), "v"(key), "v"(t[i]));
+        t[i] = r;
     }
+    t[0] = min(t[0], key);
 }
 
 struct MatchArgs {
@@ -2982,36 +2986,73 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
     KM_T(1);
     // rank F2 candidates by traversal key -> slot.  16-wave launches with few candidates: LPK
     // adjacent lanes per key, each counting every LPK-th key, summed on DPP (one thread per key
-    // counted all n2c keys: ~3.5 us per pair alone at 217 candidates)
+    // counted all n2c keys).  Every global read of this stage (the candidates' records and
+    // descriptors, the queries' records and positions, phase 1's query descriptors: host memory
+    // in a host call) is issued before the counting, so their latencies overlap it and each other
+    // instead of following one another (phase 1's then starts with its descriptors in registers;
+    // with the med3 top-8 and the row-only window test, phase 1 11.2 -> 8.2 us per pair alone)
     int lpk = 1;
     if constexpr (!BIG && NT == 1024) lpk = n2c <= 256 ? 4 : n2c <= 512 ? 2 : 1;
+    constexpr bool early = !BIG && NT == 1024;
+    uint32_t d1pre[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    orb_keypoint_t qkp{};
+    float2 qprev = make_float2(0.f, 0.f);
+    const bool qEarly = early && n1c <= NT && tid < n1c;
+    if constexpr (early) {
+        const int qP = tid / (NT / 256);  // phase 1's first round: NT / 256 lanes per query
+        if (qP < n1c) {
+            const int i1 = s_q2i[qP];
+#pragma unroll
+            for (int w = 0; w < 2; ++w) {
+                const uint4 v4 = ((const uint4*)D1)[(long long)i1 * 2 + w];
+                d1pre[4 * w] = v4.x, d1pre[4 * w + 1] = v4.y, d1pre[4 * w + 2] = v4.z, d1pre[4 * w + 3] = v4.w;
+            }
+        }
+        if (qEarly) {
+            const int i1 = s_q2i[tid];
+            qkp = K1[i1];
+            if (prev) qprev = *(const float2*)(prev + ((long long)p * cap + i1) * 2);
+        }
+    }
     for (int t0 = tid; t0 < n2c * lpk; t0 += NT) {
         const int t = t0 / lpk, sub = t0 - t * lpk;  // (lpk divides NT: a key's lanes share a wave)
         const uint32_t k = s_key[t];
+        const int i2 = (int)(k & 0xFFFF);
+        orb_keypoint_t kp{};
+        if (sub == 0) kp = K2[i2];
+        uint32_t dv[8];
+#pragma unroll
+        for (int w = 0; w < 8; ++w)
+            if (w % lpk == sub) dv[w] = D2[(long long)i2 * 8 + w];
         int rank = 0;
         for (int u = sub; u < n2c; u += lpk) rank += s_key[u] < k;
-        if constexpr (!BIG && NT == 1024) {
+        if constexpr (early) {
             if (lpk >= 2) rank += __builtin_amdgcn_mov_dpp(rank, 0xB1, 0xF, 0xF, false);  // quad_perm xor 1
             if (lpk >= 4) rank += __builtin_amdgcn_mov_dpp(rank, 0x4E, 0xF, 0xF, false);  // quad_perm xor 2
         }
+#pragma unroll
+        for (int w = 0; w < 8; ++w)
+            if (w % lpk == sub) s_d2[rank * 8 + w] = dv[w];
         if (sub != 0) continue;
-        const int i2 = (int)(k & 0xFFFF);
-        const orb_keypoint_t kp = K2[i2];
         s_x2[rank] = kp.x;
         s_y2[rank] = kp.y;
         s_a2[rank] = kp.angle;
         s_cell[rank] = (int)(k >> 16);
         s_st[rank] = make_uint2(0xFFFFu, (uint32_t)i2);
-#pragma unroll
-        for (int w = 0; w < 8; ++w) s_d2[rank * 8 + w] = D2[(long long)i2 * 8 + w];
     }
-    for (int q = tid; q < n1c; q += NT) {
-        const int i1 = s_q2i[q];
-        const orb_keypoint_t kp = K1[i1];
-        s_qx[q] = prev ? prev[((long long)p * cap + i1) * 2] : kp.x;
-        s_qy[q] = prev ? prev[((long long)p * cap + i1) * 2 + 1] : kp.y;
-        if constexpr (!BIG) s_qa[q] = kp.angle;  // (only queries are ever accepted)
+    if (qEarly) {
+        s_qx[tid] = prev ? qprev.x : qkp.x;
+        s_qy[tid] = prev ? qprev.y : qkp.y;
+        if constexpr (!BIG) s_qa[tid] = qkp.angle;
     }
+    if (!qEarly || !early)
+        for (int q = (early && n1c <= NT) ? n1c : tid; q < n1c; q += NT) {
+            const int i1 = s_q2i[q];
+            const orb_keypoint_t kp = K1[i1];
+            s_qx[q] = prev ? prev[((long long)p * cap + i1) * 2] : kp.x;
+            s_qy[q] = prev ? prev[((long long)p * cap + i1) * 2 + 1] : kp.y;
+            if constexpr (!BIG) s_qa[q] = kp.angle;  // (only queries are ever accepted)
+        }
     if constexpr (BIG) __threadfence_block();
     __syncthreads();
     for (int i = tid; i < n1; i += NT) {
@@ -3030,6 +3071,13 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
         s_col[tid] = lo;
     }
     __syncthreads();
+    // A slot in the window's column range [s_col[minCX], s_col[maxCX + 1]) already has its grid
+    // column inside the window: only its grid row is tested, so the LDS body keeps the row alone
+    // (no division by 48 per candidate)
+    if constexpr (!BIG) {
+        for (int j = tid; j < n2c; j += NT) s_cell[j] = s_cell[j] % 48;
+        __syncthreads();
+    }
     KM_T(2);
     // ---- phase 1: per-query top-8 (dist, order), two lanes per query (candidates j of one
     // parity each), their sorted lists merged on DPP ----
@@ -3046,11 +3094,16 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
             maxCX = min(63, (int)ceilf((qx - mg.minX + r) * mg.invW));
             minCY = max(0, (int)floorf((qy - mg.minY - r) * mg.invH));
             maxCY = min(47, (int)ceilf((qy - mg.minY + r) * mg.invH));
-            const int i1 = s_q2i[q];
+            if (early && q0 == 0) {
 #pragma unroll
-            for (int w = 0; w < 2; ++w) {  // two 16-B loads (descriptor rows are 32-B aligned)
-                const uint4 v4 = ((const uint4*)D1)[(long long)i1 * 2 + w];
-                d1[4 * w] = v4.x, d1[4 * w + 1] = v4.y, d1[4 * w + 2] = v4.z, d1[4 * w + 3] = v4.w;
+                for (int w = 0; w < 8; ++w) d1[w] = d1pre[w];
+            } else {
+                const int i1 = s_q2i[q];
+#pragma unroll
+                for (int w = 0; w < 2; ++w) {  // two 16-B loads (descriptor rows are 32-B aligned)
+                    const uint4 v4 = ((const uint4*)D1)[(long long)i1 * 2 + w];
+                    d1[4 * w] = v4.x, d1[4 * w + 1] = v4.y, d1[4 * w + 2] = v4.z, d1[4 * w + 3] = v4.w;
+                }
             }
         }
         uint32_t top[MATCH_TOPK];
@@ -3066,8 +3119,12 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
             const int cell = s_cell[j];
             const float x2 = s_x2[j], y2 = s_y2[j];
             const uint4 da = *(const uint4*)(s_d2 + j * 8), db = *(const uint4*)(s_d2 + j * 8 + 4);
-            const int cx = cell / 48, cy = cell - cx * 48;
-            if (cx < minCX || cx > maxCX || cy < minCY || cy > maxCY) continue;
+            if constexpr (BIG) {
+                const int cx = cell / 48, cy = cell - cx * 48;
+                if (cx < minCX || cx > maxCX || cy < minCY || cy > maxCY) continue;
+            } else {
+                if (cell < minCY || cell > maxCY) continue;  // (the grid row)
+            }
             if (fabsf(x2 - qx) > r || fabsf(y2 - qy) > r) continue;
             const int dist = __popc(d1[0] ^ da.x) + __popc(d1[1] ^ da.y) + __popc(d1[2] ^ da.z) + __popc(d1[3] ^ da.w) +
                              __popc(d1[4] ^ db.x) + __popc(d1[5] ^ db.y) + __popc(d1[6] ^ db.z) + __popc(d1[7] ^ db.w);
@@ -3142,8 +3199,12 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
         const int j1 = s_col[max(maxCX + 1, 0)];
         for (int j = s_col[min(minCX, 64)] + lane; j < j1; j += 64) {
             const int cell = s_cell[j];
-            const int cx = cell / 48, cy = cell - cx * 48;
-            if (cx < minCX || cx > maxCX || cy < minCY || cy > maxCY) continue;
+            if constexpr (BIG) {
+                const int cx = cell / 48, cy = cell - cx * 48;
+                if (cx < minCX || cx > maxCX || cy < minCY || cy > maxCY) continue;
+            } else {
+                if (cell < minCY || cell > maxCY) continue;  // (the grid row)
+            }
             if (fabsf(s_x2[j] - qx) > r || fabsf(s_y2[j] - qy) > r) continue;
             const int dist = hamming256(d1, s_d2 + j * 8);
             if (!live(j, dist)) continue;
@@ -3387,36 +3448,30 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
             atomicAdd(&s_hist[rot_bin30((BIG ? K1[i].angle : s_qa[t]) - s_a2[sl])], 1);
         }
         __syncthreads();
-        if (tid == 0) {  // ComputeThreeMaxima (ORBmatcher.cc:1748-1789)
-            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
-            for (int i = 0; i < 30; ++i) {
-                const int sz = s_hist[i];
-                if (sz > max1) {
-                    max3 = max2;
-                    max2 = max1;
-                    max1 = sz;
-                    ind3 = ind2;
-                    ind2 = ind1;
-                    ind1 = i;
-                } else if (sz > max2) {
-                    max3 = max2;
-                    max2 = sz;
-                    ind3 = ind2;
-                    ind2 = i;
-                } else if (sz > max3) {
-                    max3 = sz;
-                    ind3 = i;
-                }
-            }
+        if (wave == 0) {
+            // ComputeThreeMaxima (ORBmatcher.cc:1748-1789) on one wave: its strict-> insertion scan
+            // keeps the three largest non-zero counts, ties in bin order, so the bins are the
+            // three largest keys (count << 8 | 255 - bin) by wave-max reductions (tid 0 scanning
+            // the 30 bins took ~1 us per pair)
+            const int v = lane < 30 ? s_hist[lane] : 0;
+            const uint32_t key = v > 0 ? ((uint32_t)v << 8) | (uint32_t)(255 - lane) : 0u;
+            const uint32_t k1 = ~wave_min_u32(~key);
+            const uint32_t k2 = ~wave_min_u32(~(key == k1 ? 0u : key));
+            const uint32_t k3 = ~wave_min_u32(~(key == k1 || key == k2 ? 0u : key));
+            const int max1 = (int)(k1 >> 8), max2 = (int)(k2 >> 8), max3 = (int)(k3 >> 8);
+            int ind1 = k1 ? 255 - (int)(k1 & 255u) : -1, ind2 = k2 ? 255 - (int)(k2 & 255u) : -1;
+            int ind3 = k3 ? 255 - (int)(k3 & 255u) : -1;
             if (max2 < 0.1f * (float)max1) {
                 ind2 = -1;
                 ind3 = -1;
             } else if (max3 < 0.1f * (float)max1) {
                 ind3 = -1;
             }
-            s_ind[0] = ind1;
-            s_ind[1] = ind2;
-            s_ind[2] = ind3;
+            if (lane == 0) {
+                s_ind[0] = ind1;
+                s_ind[1] = ind2;
+                s_ind[2] = ind3;
+            }
         }
         __syncthreads();
         const int i1x = s_ind[0], i2x = s_ind[1], i3x = s_ind[2];

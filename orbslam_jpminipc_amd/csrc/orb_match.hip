@@ -196,13 +196,17 @@ __device__ __forceinline__ void load_desc(const uint32_t* p, uint32_t (&d)[8]) {
 }
 __device__ __forceinline__ uint32_t wave_min(uint32_t v) { return orbdev::wave_min_u32(v); }
 __device__ __forceinline__ int wave_sum(int v) { return orbdev::wave_total(v); }
+// Insert key into the sorted list t, keeping the smallest entries: the new t[i] is the median
+// of (old t[i-1], key, old t[i]) -- one v_med3_u32 per entry, all independent (the min / max
+// insertion chain was two dependent ops per entry)
 __device__ __forceinline__ void topk_insert(uint32_t (&t)[TOPK], uint32_t key) {
 #pragma unroll
-    for (int i = 0; i < TOPK; ++i) {
-        const uint32_t lo = min(t[i], key), hi = max(t[i], key);
-        t[i] = lo;
-        key = hi;
+    for (int i = TOPK - 1; i >= 1; --i) {
+        uint32_t r;
+        asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(t[i - 1]), "v"(key), "v"(t[i]));
+        t[i] = r;
     }
+    t[0] = min(t[0], key);
 }
 
 // ---- k_grid_build ------------------------------------------------------------------------
