@@ -2144,7 +2144,27 @@ __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, G
     // ((y-16) / cellH, (x-16) / cellW) by exact reciprocal multiplies (host-checked).
     int* fcount = cellCount + (long long)b * g.nCells + lg.cell0;
     uint32_t* fcand = cand + (long long)b * g.candPerFrame + lg.candBase;
-    auto nms_emit = [&](const uint16_t* list, int n) {  // list == pq, or a list disjoint from it
+    // the tile's cells: rows ciT0 .. ciT1, columns cjT0 .. cjT0 + ncT - 1 (wave-uniform)
+    const int ciT0 = (int)__umulhi((uint32_t)(t.y0 - EDGE), (uint32_t)lg.cellHm);
+    const int ciT1 = (int)__umulhi((uint32_t)(t.y0 + t.th - 1 - EDGE), (uint32_t)lg.cellHm);
+    const int cjT0 = (int)__umulhi((uint32_t)(t.x0 - EDGE), (uint32_t)lg.cellWm);
+    const int cjT1 = (int)__umulhi((uint32_t)(min(t.x0 + 4 * t.tw4, lg.detX1) - 1 - EDGE), (uint32_t)lg.cellWm);
+    const int ncT = cjT1 - cjT0 + 1, nT = (ciT1 - ciT0 + 1) * ncT;
+    // KF_AGG: the survivors' cell slots taken per workgroup -- an LDS count per cell of the tile,
+    // one global atomicAdd per cell, each survivor at the cell's base + its LDS rank -- instead of
+    // one returning global atomic per survivor on the few counters of the tile's cells (their
+    // same-address serialisation at L2 cost ~0.05 ms per c3 step: timing ablation `kf_noemit`,
+    // profiles/r06/r06_w_summary.txt).  The counts and bases overlay s_px, the ranks s_in (both
+    // free after the strength passes).
+#ifndef KF_AGG
+#define KF_AGG 1
+#endif
+    int* s_cc = (int*)s_px[0];
+    int* s_base = s_cc + 64;
+    uint16_t* s_rk = (uint16_t*)s_in;
+    static_assert(sizeof(s_px) >= 128 * sizeof(int) && FT_IN_BYTES >= 4 * FT_CL * 2, "KF_AGG's LDS overlays");
+    auto nms_emit = [&](const uint16_t* list, int n, auto aggC) {  // list == pq, or a list disjoint from it
+        constexpr bool AGG = decltype(aggC)::value;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         int sn = 0;
         for (int k0 = 0; k0 < n; k0 += 64) {
@@ -2193,20 +2213,47 @@ __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, G
             const uint16_t e = pq[k];
             const int rt = e >> 9, ct = e & 511;
             const int X = t.x0 + ct, Y = t.y0 + rt;
-            const int c = (int)__umulhi((uint32_t)(Y - EDGE), (uint32_t)lg.cellHm) * lg.cols +
-                          (int)__umulhi((uint32_t)(X - EDGE), (uint32_t)lg.cellWm);
-            const int S = s_S[(rt + 1) * spw + ct + 4];
-            const int pos = atomicAdd(fcount + c, 1);
-            if (pos < lg.capMax)
-                fcand[c * lg.capMax + pos] = ((uint32_t)(S - 1) << 24) | ((uint32_t)Y << 12) | (uint32_t)X;
+            const int ci = (int)__umulhi((uint32_t)(Y - EDGE), (uint32_t)lg.cellHm);
+            const int cj = (int)__umulhi((uint32_t)(X - EDGE), (uint32_t)lg.cellWm);
+            if constexpr (AGG) {
+                s_rk[wave * FT_CL + k] = (uint16_t)atomicAdd(&s_cc[(ci - ciT0) * ncT + (cj - cjT0)], 1);
+            } else {
+                const int c = ci * lg.cols + cj;
+                const int S = s_S[(rt + 1) * spw + ct + 4];
+                const int pos = atomicAdd(fcount + c, 1);
+                if (pos < lg.capMax)
+                    fcand[c * lg.capMax + pos] = ((uint32_t)(S - 1) << 24) | ((uint32_t)Y << 12) | (uint32_t)X;
+            }
         }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        return sn;
     };
     // the NMS on the wave's own corner list (filled by its strength passes), or, where a wave's
     // list overflowed, on the plane's interior corners (ballot-compacted, flattened over th x
     // tw4 dwords) by all waves
-    if (!s_ovf) {
-        if (ncl) nms_emit(cl, ncl);
+    if (KF_AGG && !s_ovf && nT <= 64) {  // (workgroup-uniform)
+        if (tid < 64) s_cc[tid] = 0;
+        __syncthreads();
+        const int sn = ncl ? nms_emit(cl, ncl, std::true_type{}) : 0;
+        __syncthreads();
+        if (tid < nT) {
+            const int cnt = s_cc[tid];
+            if (cnt) s_base[tid] = atomicAdd(fcount + (ciT0 + tid / ncT) * lg.cols + cjT0 + tid % ncT, cnt);
+        }
+        __syncthreads();
+        for (int k = lane; k < sn; k += 64) {
+            const uint16_t e = pq[k];
+            const int rt = e >> 9, ct = e & 511;
+            const int X = t.x0 + ct, Y = t.y0 + rt;
+            const int ci = (int)__umulhi((uint32_t)(Y - EDGE), (uint32_t)lg.cellHm);
+            const int cj = (int)__umulhi((uint32_t)(X - EDGE), (uint32_t)lg.cellWm);
+            const int S = s_S[(rt + 1) * spw + ct + 4];
+            const int pos = s_base[(ci - ciT0) * ncT + (cj - cjT0)] + s_rk[wave * FT_CL + k];
+            if (pos < lg.capMax)
+                fcand[(ci * lg.cols + cj) * lg.capMax + pos] = ((uint32_t)(S - 1) << 24) | ((uint32_t)Y << 12) | (uint32_t)X;
+        }
+    } else if (!s_ovf) {
+        if (ncl) nms_emit(cl, ncl, std::false_type{});
     } else {
         int cn = 0;
         const int nI = t.th * t.tw4;
@@ -2228,11 +2275,11 @@ __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, G
                 cn += __popcll(m);
             }
             if (cn > FT_Q - 256) {
-                nms_emit(pq, cn);
+                nms_emit(pq, cn, std::false_type{});
                 cn = 0;
             }
         }
-        if (cn) nms_emit(pq, cn);
+        if (cn) nms_emit(pq, cn, std::false_type{});
     }
 #if KF_TIMING
     KF_T(5);
@@ -2789,6 +2836,9 @@ struct MatchGeom {
 #ifndef KM_FIX
 #define KM_FIX 1  // 0: the sequential (speculated) phase 2 for every launch
 #endif
+#ifndef KM_FIX_BATCH
+#define KM_FIX_BATCH 0  // 1: the fixed point in the batched (8-wave) launches too
+#endif
 #ifndef KM_TIMING  // 1: per-phase s_memrealtime sums of k_match_init's pairs (experiment builds only)
 #define KM_TIMING 0
 #endif
@@ -3249,8 +3299,8 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
     // Final: every accepting query keeps its slot (bins count the stolen ones too), the slot's
     // last acceptor owns the match (vnMatches21).
     bool fixDone = false;
-    if constexpr (!BIG && NT == 1024) {
-        if (A.fixOff) {
+    if constexpr (!BIG) {
+        if (A.fixOff) {  // (the host enables it only when every query has a thread: nmax <= NT)
             __shared__ int s_fn, s_fch, s_fovf;
             uint32_t* faB[2];
             int* fcB[2];
@@ -4936,7 +4986,8 @@ static int sfi_launch(const orb_keypoint_t* d_kps, const uint8_t* d_desc, const 
     int fixOff = 0;
     const size_t fixAt = (match_lds_bytes(cap, nmax) + 15) & ~(size_t)15;
     const size_t fixEnd = fixAt + (size_t)nmax * (2 * 16 + 8 + 2);
-    if (P < KM_WIDE_PAIRS && KM_FIX && fixEnd <= 158 * 1024) {
+    const int ntLaunch = P < KM_WIDE_PAIRS ? 2 * KM_THREADS : KM_THREADS;
+    if (KM_FIX && (P < KM_WIDE_PAIRS || KM_FIX_BATCH) && nmax <= ntLaunch && fixEnd <= 158 * 1024) {
         fixOff = (int)fixAt;
         lds = std::max(lds, fixEnd);
     }
