@@ -2836,6 +2836,12 @@ struct MatchGeom {
 #ifndef KM_FIX
 #define KM_FIX 1  // 0: the sequential (speculated) phase 2 for every launch
 #endif
+#ifndef KM_WIDE_PHASE0
+#define KM_WIDE_PHASE0 1  // phase 0's compaction by the whole workgroup (every launch)
+#endif
+#ifndef KM_EARLY_BATCH
+#define KM_EARLY_BATCH 1  // the staging reads ahead of the ranking in 8-wave launches too
+#endif
 #ifndef KM_FIX_BATCH
 #define KM_FIX_BATCH 0  // 1: the fixed point in the batched (8-wave) launches too
 #endif
@@ -2971,10 +2977,10 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
     for (int i = tid; i < n1; i += NT) s_m12[i] = K1[i].octave == 0;  // level1 > 0 -> continue (ORBmatcher.cc:615)
     if constexpr (BIG) __threadfence_block();
     __syncthreads();
-    if constexpr (!BIG && NT == 1024) {
-        // 16 waves: both lists compacted by the whole workgroup, 1024 entries per round (per wave
-        // a ballot count, the waves' offsets from a 16-entry table); the single-wave loops
-        // below took ~2.6 us per pair alone
+    if constexpr (!BIG && KM_WIDE_PHASE0) {
+        // both lists compacted by the whole workgroup, NT entries per round (per wave a ballot
+        // count, the waves' offsets from a table of NT / 64); the single-wave loops below took
+        // ~2.6 us per pair alone
         __shared__ int s_wc2[16], s_wc1[16];
         int base2 = 0, base1 = 0;
         for (int i0 = 0; i0 < max(n1, n2); i0 += NT) {
@@ -2989,7 +2995,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
             }
             __syncthreads();  // (also: every read of s_key's round precedes the writes below)
             int o2 = base2, o1 = base1, t2 = 0, t1 = 0;
-            for (int w = 0; w < 16; ++w) {
+            for (int w = 0; w < NT / 64; ++w) {
                 const int c2 = s_wc2[w], c1 = s_wc1[w];
                 if (w < wave) o2 += c2, o1 += c1;
                 t2 += c2;
@@ -3043,7 +3049,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
     // with the med3 top-8 and the row-only window test, phase 1 11.2 -> 8.2 us per pair alone)
     int lpk = 1;
     if constexpr (!BIG && NT == 1024) lpk = n2c <= 256 ? 4 : n2c <= 512 ? 2 : 1;
-    constexpr bool early = !BIG && NT == 1024;
+    constexpr bool early = !BIG && (NT == 1024 || KM_EARLY_BATCH);
     uint32_t d1pre[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
     orb_keypoint_t qkp{};
     float2 qprev = make_float2(0.f, 0.f);
