@@ -14,7 +14,7 @@ import sys
 
 import numpy as np
 
-ROOT = pathlib.Path(__file__).resolve().parent.parent
+ROOT = pathlib.Path(__file__).resolve().parents[2]
 OD_WP, OD_HN, OD_WR, HALF = 64, 56, 21, 15
 KOD = (0, 16, 28)
 

@@ -6,7 +6,7 @@ import sys
 import time
 import pathlib
 
-ROOT = pathlib.Path(__file__).resolve().parent.parent
+ROOT = pathlib.Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT))
 import torch  # noqa: E402
 

@@ -107,7 +107,8 @@ PY
             ./build/latency_gpu 640 480 1000 50 > "$OUT/latprof.log" 2>&1
         rc=$?; fin latprof $rc fatal ;;
     py)  # py:SCRIPT:ARGS  python scripts/SCRIPT with comma-separated ARGS
-        f=$OUT/py_${a%.py}_${b//[^A-Za-z0-9]/_}.txt
+        n=${a%.py}
+        f=$OUT/py_${n//\//_}_${b//[^A-Za-z0-9]/_}.txt
         timeout -k 10 300 python "scripts/$a" ${b//,/ } > "$f" 2>&1
         rc=$?; grep -v amdgpu.ids "$f" | tail -4 | tee -a "$OUT/summary.txt"; fin "$S" $rc fatal ;;
     bin)  # bin:NAME  build/NAME (a probe built on the CPU side)
