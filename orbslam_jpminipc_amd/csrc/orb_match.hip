@@ -1473,6 +1473,19 @@ int run_job(const Call& C, const Job& J) {
         hipLaunchKernelGGL(k_query_prep, dim3((J.qn + 255) / 256), dim3(256), 0, s, J);
         hipLaunchKernelGGL(k_query_scan, dim3((J.qn + 3) / 4), dim3(256), 0, s, J);
     }
+    // SearchByProjection(local): the fixed-point resolver where its state fits (it also takes
+    // targets k_resolve's per-target LDS state cannot: 8 B per target instead of 13)
+    if (J.mode == M_LOCAL && resolve_fix_lds(J) <= 150 * 1024) {
+        static std::atomic<bool> fix_attr[64] = {};
+        if (!fix_attr[C.device].load()) {
+            HIPCHK(hipFuncSetAttribute((const void*)k_resolve_fix<M_LOCAL>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       150 * 1024));
+            fix_attr[C.device] = true;
+        }
+        hipLaunchKernelGGL(k_resolve_fix<M_LOCAL>, dim3(1), dim3(RF_THREADS), resolve_fix_lds(J), s, J);
+        HIPCHK(hipGetLastError());
+        return ORB_OK;
+    }
     size_t lds = 0;
     int st = resolve_lds(J, &lds);
     if (st) return st;
@@ -1493,17 +1506,6 @@ int run_job(const Call& C, const Job& J) {
         SET_RESOLVE_LDS(M_TRIANG);
 #undef SET_RESOLVE_LDS
         attr_set[C.device] = true;
-    }
-    if (J.mode == M_LOCAL && resolve_fix_lds(J) <= 150 * 1024) {
-        static std::atomic<bool> fix_attr[64] = {};
-        if (!fix_attr[C.device].load()) {
-            HIPCHK(hipFuncSetAttribute((const void*)k_resolve_fix<M_LOCAL>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       150 * 1024));
-            fix_attr[C.device] = true;
-        }
-        hipLaunchKernelGGL(k_resolve_fix<M_LOCAL>, dim3(1), dim3(RF_THREADS), resolve_fix_lds(J), s, J);
-        HIPCHK(hipGetLastError());
-        return ORB_OK;
     }
     switch (J.mode) {
 #define LAUNCH_RESOLVE(M) \

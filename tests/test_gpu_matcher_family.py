@@ -74,6 +74,32 @@ def test_search_by_projection_local(seed, th):
     assert n > 0
 
 
+@pytest.mark.parametrize("n_kp,n_mp", [(16000, 3000), (11000, 17000), (2500, 2500)])
+def test_search_by_projection_local_large(n_kp, n_mp):
+    """Frames near the target-frame limit (MAX_TARGET = 16384 keypoints): k_grid_build's LDS
+    counting sort over several 1024-entry rounds (u16 item indices), and SearchByProjection
+    (local) through the fixed-point resolver (takenBy + queries within its 150 KB of LDS: 16000
+    targets, which the sequential resolver's 13 B per target cannot hold) or, past it (11000
+    targets + 17000 points), through the speculated sequential resolver."""
+    rng = np.random.default_rng(900 + n_kp + n_mp)
+    F = S.view(rng, n_kp, clusters=40)
+    mps, _ = S.map_points_on(rng, F, n_mp)
+    g, o = both(0.8)
+    iv, px, py, lv, vc = o.isInFrustum(F, mps, 0.5)
+    taken = (rng.random(F.n) < 0.1).astype(np.uint8)
+    usable = iv & (rng.random(mps.n) < 0.95)
+    n = same(g.SearchByProjection_Local(F, taken, usable, px, py, lv, vc, mps.desc, 2.0),
+             o.SearchByProjection_Local(F, taken, usable, px, py, lv, vc, mps.desc, 2.0))
+    assert n > 0
+    q = 200
+    x = rng.uniform(0, S.W, q).astype(np.float32)
+    y = rng.uniform(0, S.H, q).astype(np.float32)
+    r = rng.uniform(0, 40, q).astype(np.float32)
+    gi = orb.ORBmatcher.GetFeaturesInArea(F, x, y, r, None, None, True)
+    for i in range(0, q, 17):
+        np.testing.assert_array_equal(gi[i], o.GetFeaturesInArea(F, x[i], y[i], r[i], -1, -1, True))
+
+
 @pytest.mark.parametrize("seed", SEEDS)
 @pytest.mark.parametrize("window,lv", [(100, (0, 2**31 - 1)), (200, (1, 5)), (30, (0, 2**31 - 1))])
 def test_window_search(seed, window, lv):
