@@ -1012,9 +1012,11 @@ __global__ void __launch_bounds__(256) k_resolve(Job J) {
     if (tid == 0) J.nOut[0] = s_nacc;
 }
 
-// SearchByProjection (local map, ORBmatcher.cc:49-125) without a sequential pass.  A query's
-// decision is a function of which of its candidates earlier queries took (`F.mvpMapPoints[idx]`
-// set earlier in the loop, ORBmatcher.cc:87-88): with takenBy[t] = the smallest query that
+// The projection-family matchers without a sequential pass: SearchByProjection (local map,
+// ORBmatcher.cc:49-125; motion 1507-1620; relocalisation 1622-1746; Sim3 286-407; frame to
+// frame 519-594) and WindowSearch (409-516).  A query's decision is a function of which of its
+// candidates earlier queries took (e.g. `F.mvpMapPoints[idx]` set earlier in the loop,
+// ORBmatcher.cc:87-88): with takenBy[t] = the smallest query that
 // accepted target t (-1: taken before the call), query q sees t taken iff takenBy[t] < q.  Every
 // query is decided in parallel from the previous iteration's takenBy, the accepted targets give
 // the next takenBy (atomicMin), until takenBy repeats.  The sequential result is the unique
@@ -1026,10 +1028,17 @@ __global__ void __launch_bounds__(256) k_resolve(Job J) {
 // The loop is bounded by qn + 2 iterations (the induction's bound + the one that sees no
 // change); past it the kernel reports -1 matches and the call fails (cannot happen).
 #define RF_THREADS 1024
+#ifndef RF_ALL_MODES
+#define RF_ALL_MODES 1  // 0: the fixed point for SearchByProjection(local) only
+#endif
 size_t resolve_fix_lds(const Job& J) { return (size_t)2 * std::max(J.T.n, 1) * 4 + (size_t)std::max(J.qn, 1) * 4 + 16; }
 template <int MODE>
 __global__ void __launch_bounds__(RF_THREADS) k_resolve_fix(Job J) {
-    static_assert(MODE == M_LOCAL, "the fixed-point resolver covers SearchByProjection(local)");
+    // the projection-family matchers whose only loop-carried state is the taken targets (each
+    // reports by target: out[target] = query)
+    static_assert(MODE == M_LOCAL || MODE == M_WINDOW || MODE == M_F2F || MODE == M_MOTION || MODE == M_RELOC ||
+                      MODE == M_SIM3P,
+                  "fixed-point resolver mode");
     extern __shared__ __attribute__((aligned(16))) int rsm[];
     __shared__ int s_changed, s_nres, s_nacc;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1100,13 +1109,62 @@ __global__ void __launch_bounds__(RF_THREADS) k_resolve_fix(Job J) {
         done = s_changed == 0;
         __syncthreads();  // s_changed read by all before the next iteration resets it
     }
+    // the rotation consistency check of the matchers that have one (e.g. ORBmatcher.cc:491-512):
+    // the histogram counts every final acceptance, order-free
+    __shared__ int s_hist[HISTO + 2];
+    __shared__ int s_ind[3];
+    const bool rotMode = J.checkOri && (MODE == M_WINDOW || MODE == M_MOTION || MODE == M_RELOC);
     if (tid == 0) s_nacc = 0;
+    if (rotMode) {
+        if (tid < HISTO) s_hist[tid] = 0;
+        __syncthreads();
+        for (int t = tid; t < Tn; t += RF_THREADS) {
+            const int v = s_tb[t];
+            if (v >= 0 && v != INT_MAX) atomicAdd(&s_hist[rot_bin(J.qkps[qrow(J, v)].angle, J.T.kps[t].angle)], 1);
+        }
+        __syncthreads();
+        if (tid == 0) {  // ComputeThreeMaxima (1748-1789)
+            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+            for (int i = 0; i < HISTO; ++i) {
+                const int sz = s_hist[i];
+                if (sz > max1) {
+                    max3 = max2;
+                    max2 = max1;
+                    max1 = sz;
+                    ind3 = ind2;
+                    ind2 = ind1;
+                    ind1 = i;
+                } else if (sz > max2) {
+                    max3 = max2;
+                    max2 = sz;
+                    ind3 = ind2;
+                    ind2 = i;
+                } else if (sz > max3) {
+                    max3 = sz;
+                    ind3 = i;
+                }
+            }
+            if (max2 < 0.1f * (float)max1) {
+                ind2 = -1;
+                ind3 = -1;
+            } else if (max3 < 0.1f * (float)max1) {
+                ind3 = -1;
+            }
+            s_ind[0] = ind1;
+            s_ind[1] = ind2;
+            s_ind[2] = ind3;
+        }
+    }
     __syncthreads();
     int acc = 0;
     for (int t = tid; t < J.outN; t += RF_THREADS) {  // outN == Tn (by target)
         const int v = s_tb[t];
-        const bool a = v >= 0 && v != INT_MAX;
-        J.out[t] = a ? v : -1;
+        bool a = v >= 0 && v != INT_MAX;
+        if (a && rotMode) {
+            const int bn = rot_bin(J.qkps[qrow(J, v)].angle, J.T.kps[t].angle);
+            a = bn == s_ind[0] || bn == s_ind[1] || bn == s_ind[2];
+        }
+        J.out[t] = a ? qrow(J, v) : -1;
         acc += a;
     }
     acc = wave_sum(acc);
@@ -1475,14 +1533,36 @@ int run_job(const Call& C, const Job& J) {
     }
     // SearchByProjection(local): the fixed-point resolver where its state fits (it also takes
     // targets k_resolve's per-target LDS state cannot: 8 B per target instead of 13)
-    if (J.mode == M_LOCAL && resolve_fix_lds(J) <= 150 * 1024) {
+    const bool fixMode = J.outByTarget && (J.mode == M_LOCAL || (RF_ALL_MODES && (J.mode == M_WINDOW || J.mode == M_F2F ||
+                                                                                   J.mode == M_MOTION || J.mode == M_RELOC ||
+                                                                                   J.mode == M_SIM3P)));
+    if (fixMode && resolve_fix_lds(J) <= 150 * 1024) {
         static std::atomic<bool> fix_attr[64] = {};
         if (!fix_attr[C.device].load()) {
-            HIPCHK(hipFuncSetAttribute((const void*)k_resolve_fix<M_LOCAL>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       150 * 1024));
+#define SET_FIX_LDS(M) HIPCHK(hipFuncSetAttribute((const void*)k_resolve_fix<M>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024))
+            SET_FIX_LDS(M_LOCAL);
+            SET_FIX_LDS(M_WINDOW);
+            SET_FIX_LDS(M_F2F);
+            SET_FIX_LDS(M_MOTION);
+            SET_FIX_LDS(M_RELOC);
+            SET_FIX_LDS(M_SIM3P);
+#undef SET_FIX_LDS
             fix_attr[C.device] = true;
         }
-        hipLaunchKernelGGL(k_resolve_fix<M_LOCAL>, dim3(1), dim3(RF_THREADS), resolve_fix_lds(J), s, J);
+        const size_t fl = resolve_fix_lds(J);
+        switch (J.mode) {
+#define LAUNCH_FIX(M) \
+    case M: hipLaunchKernelGGL(k_resolve_fix<M>, dim3(1), dim3(RF_THREADS), fl, s, J); break;
+            LAUNCH_FIX(M_LOCAL)
+            LAUNCH_FIX(M_WINDOW)
+            LAUNCH_FIX(M_F2F)
+            LAUNCH_FIX(M_MOTION)
+            LAUNCH_FIX(M_RELOC)
+            LAUNCH_FIX(M_SIM3P)
+#undef LAUNCH_FIX
+            default:
+                return fail(ORB_EINVAL, "matcher mode without a fixed-point resolver");
+        }
         HIPCHK(hipGetLastError());
         return ORB_OK;
     }

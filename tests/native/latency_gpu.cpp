@@ -118,6 +118,21 @@ int main(int argc, char** argv) {
     std::vector<int32_t> lvl(n1);
     for (int i = 0; i < n1; ++i) px[i] = k[0][i].x, py[i] = k[0][i].y, lvl[i] = k[0][i].octave;
     std::vector<int32_t> sbp(n2);
+    // SearchByProjection(motion model), Tracking.cc:1078 (monocular th = 15): the last frame's
+    // keypoints as map points at depth 5 in front of identical poses, so each projects where it
+    // was detected; WindowSearch (ORBmatcher.cc:409-516) between the two frames, window 100
+    const float fx = V1.fx, fy = V1.fy, cx = V1.cx, cy = V1.cy;
+    std::vector<float> mpos((size_t)n1 * 3);
+    for (int i = 0; i < n1; ++i) {
+        const float z = 5.0f;
+        mpos[3 * i] = (k[0][i].x - cx) / fx * z;
+        mpos[3 * i + 1] = (k[0][i].y - cy) / fy * z;
+        mpos[3 * i + 2] = z;
+    }
+    orb_map_points_t mp{};
+    mp.pos = mpos.data();
+    mp.n = n1;
+    std::vector<int32_t> mot(n2), win(n2);
     std::printf("{\"width\": %d, \"height\": %d, \"nfeatures\": %d, \"n1\": %d, \"n2\": %d, \"reps\": %d, ", W, H, NF,
                 n1, n2, reps);
     timeit("orb_extract", reps, [&] {
@@ -138,6 +153,14 @@ int main(int argc, char** argv) {
         int nm = 0;
         return orb_search_by_projection_local(&V2, nullptr, n1, usable.data(), px.data(), py.data(), lvl.data(),
                                               vcos.data(), d[0].data(), 1.0f, 0.9f, sbp.data(), &nm, 0);
+    }, false);
+    timeit("orb_search_by_projection_motion", reps, [&] {
+        int nm = 0;
+        return orb_search_by_projection_motion(&V2, nullptr, &V1, mp, usable.data(), 15.0f, 1, mot.data(), &nm, 0);
+    }, false);
+    timeit("orb_window_search", reps, [&] {
+        int nm = 0;
+        return orb_window_search(&V1, usable.data(), &V2, 100, 0, 7, 0.9f, 1, win.data(), &nm, 0);
     }, true);
     std::printf("}\n");
     orb_extractor_destroy(h);
