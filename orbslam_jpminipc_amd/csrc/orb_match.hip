@@ -51,6 +51,7 @@ namespace {
 
 constexpr int GRID_COLS = 64, GRID_ROWS = 48, NCELLS = GRID_COLS * GRID_ROWS;  // Frame.h:35-36
 constexpr int TOPK = 8;
+constexpr int TOPK_FIX = 32;  // the fixed-point resolver's lists (fewer exact rescans)
 constexpr int TH_HIGH = 100, TH_LOW = 50, HISTO = 30;  // ORBmatcher.cc:40-42
 constexpr int MAX_TARGET = 16384;                       // keypoints per target frame (LDS state)
 static_assert(NCELLS == 3 * 1024 && MAX_TARGET <= 65536, "k_grid_build: 3 cells per thread, u16 item indices");
@@ -140,8 +141,10 @@ struct Job {
     // state, scratch, outputs
     const uint8_t* taken0;  // T.n exclusion flags on entry (NULL = none)
     QP* qp;
-    uint32_t* topk;  // qn x TOPK
-    uint32_t* topx;  // qn x TOPK: target index | octave << 24 of each top-8 entry (k_query_scan)
+    uint32_t* topk;  // qn x topS (allocated qn x TOPK_FIX)
+    uint32_t* topx;  // qn x topS: target index | octave << 24 of each entry (k_query_scan)
+    int topS;        // list length / stride: TOPK (k_resolve) or TOPK_FIX (k_resolve_fix)
+    int* kval;       // (topS == TOPK_FIX) per query: the list's exact prefix (entries past it may be missing)
     int* cnt;        // qn
     int* out;        // outN
     int outN, outByTarget;
@@ -503,6 +506,11 @@ __device__ __forceinline__ int key_idx(const Job& J, uint32_t key) {
 }
 
 // ---- k_query_scan: one wave per query ---------------------------------------------------
+// Each lane keeps its candidates' 8 smallest keys; LK rounds of wave-min merge them into the
+// query's LK smallest.  For LK > 8 a lane may own more than 8 of them: once a lane that scanned
+// more than 8 candidates has given up its 8th, the later entries are no longer guaranteed, and
+// kval[q] records the exact prefix (the resolver rescans past it).
+template <int LK>
 __global__ void __launch_bounds__(256) k_query_scan(Job J) {
     const int q = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (q >= J.qn) return;
@@ -533,21 +541,28 @@ __global__ void __launch_bounds__(256) k_query_scan(Job J) {
             ++n;
         });
     }
+    const int nLane = n;
     n = wave_sum(n);
-    // merge the lanes' sorted lists: 8 rounds of wave-min; keys are unique per candidate
+    // merge the lanes' sorted lists: LK rounds of wave-min; keys are unique per candidate
     uint32_t res = 0xFFFFFFFFu;
+    int popped = 0, kv = LK;
 #pragma unroll
-    for (int k = 0; k < TOPK; ++k) {
+    for (int k = 0; k < LK; ++k) {
         const uint32_t mn = wave_min(top[0]);
-        if (top[0] == mn && mn != 0xFFFFFFFFu) {
+        const bool mine = top[0] == mn && mn != 0xFFFFFFFFu;
+        if (mine) {
 #pragma unroll
             for (int i = 0; i < TOPK - 1; ++i) top[i] = top[i + 1];
             top[TOPK - 1] = 0xFFFFFFFFu;
+            ++popped;
         }
         if (lane == k) res = mn;
+        if constexpr (LK > TOPK) {
+            if (__ballot(mine && popped == TOPK && nLane > TOPK) != 0ull) kv = min(kv, k + 1);
+        }
     }
-    if (lane < TOPK) {
-        J.topk[(size_t)q * TOPK + lane] = res;
+    if (lane < LK) {
+        J.topk[(size_t)q * LK + lane] = res;
         // the entry's target and its octave, so the loop-carried resolver reads no dependent
         // global data per query
         uint32_t x = 0;
@@ -555,9 +570,12 @@ __global__ void __launch_bounds__(256) k_query_scan(Job J) {
             const int idx = key_idx(J, res);
             x = (uint32_t)idx | ((uint32_t)J.T.kps[idx].octave << 24);
         }
-        J.topx[(size_t)q * TOPK + lane] = x;
+        J.topx[(size_t)q * LK + lane] = x;
     }
-    if (lane == 0) J.cnt[q] = n;
+    if (lane == 0) {
+        J.cnt[q] = n;
+        if constexpr (LK > TOPK) J.kval[q] = kv;
+    }
 }
 
 // AREA: ordered write of every candidate index (wave per query, ballot compaction)
@@ -1028,6 +1046,12 @@ __global__ void __launch_bounds__(256) k_resolve(Job J) {
 // The loop is bounded by qn + 2 iterations (the induction's bound + the one that sees no
 // change); past it the kernel reports -1 matches and the call fails (cannot happen).
 #define RF_THREADS 1024
+#ifndef RF_DEBUG
+#define RF_DEBUG 0  // 1: iterations / rescans per call printed (experiment builds)
+#endif
+#ifndef RF_TOPK
+#define RF_TOPK TOPK  // TOPK_FIX: 32-entry lists for the fixed-point resolver (fewer exact rescans)
+#endif
 #ifndef RF_ALL_MODES
 #define RF_ALL_MODES 1  // 0: the fixed point for SearchByProjection(local) only
 #endif
@@ -1049,7 +1073,13 @@ __global__ void __launch_bounds__(RF_THREADS) k_resolve_fix(Job J) {
     for (int t = tid; t < Tn; t += RF_THREADS) s_tb[t] = J.taken0 && J.taken0[t] ? -1 : INT_MAX;
     constexpr int need = needs_second(MODE) ? 2 : 1;
     bool done = false;
+#if RF_DEBUG
+    int dbgIt = 0, dbgRes = 0;
+#endif
     for (int it = 0; it < J.qn + 2 && !done; ++it) {
+#if RF_DEBUG
+        ++dbgIt;
+#endif
         for (int t = tid; t < Tn; t += RF_THREADS) s_tn[t] = J.taken0 && J.taken0[t] ? -1 : INT_MAX;
         if (tid == 0) {
             s_nres = 0;
@@ -1060,13 +1090,14 @@ __global__ void __launch_bounds__(RF_THREADS) k_resolve_fix(Job J) {
             if (!(J.qp[q].flags & 1)) continue;
             const int cnt = J.cnt[q];
             if (cnt == 0) continue;
-            const int k = min(cnt, TOPK);
+            const int kv = J.topS == TOPK_FIX ? J.kval[q] : TOPK;  // the list's exact prefix
+            const int k = min(cnt, kv);
             uint32_t b1 = 0xFFFFFFFFu, b2 = 0xFFFFFFFFu, x1 = 0u, x2 = 0u;
             int nUnt = 0;
             for (int j = 0; j < k; ++j) {
-                const uint32_t x = J.topx[(size_t)q * TOPK + j];
+                const uint32_t x = J.topx[(size_t)q * J.topS + j];
                 if (s_tb[x & 0xFFFFFFu] < q) continue;
-                const uint32_t e = J.topk[(size_t)q * TOPK + j];
+                const uint32_t e = J.topk[(size_t)q * J.topS + j];
                 if (nUnt == 0) {
                     b1 = e;
                     x1 = x;
@@ -1076,7 +1107,7 @@ __global__ void __launch_bounds__(RF_THREADS) k_resolve_fix(Job J) {
                 }
                 if (++nUnt == need) break;
             }
-            if (cnt > TOPK && nUnt < need) {
+            if (cnt > k && nUnt < need) {
                 s_res[atomicAdd(&s_nres, 1)] = q;
                 continue;
             }
@@ -1087,6 +1118,9 @@ __global__ void __launch_bounds__(RF_THREADS) k_resolve_fix(Job J) {
                 atomicMin(&s_tn[x1 & 0xFFFFFFu], q);
         }
         __syncthreads();
+#if RF_DEBUG
+        dbgRes += s_nres;
+#endif
         for (int r = wave; r < s_nres; r += RF_THREADS / 64) {  // exact rescans, a wave each
             const int q = s_res[r];
             uint32_t b1, b2;
@@ -1172,7 +1206,10 @@ __global__ void __launch_bounds__(RF_THREADS) k_resolve_fix(Job J) {
     __syncthreads();
     if (tid == 0) {
         J.nOut[0] = done ? s_nacc : -1;
-        J.nOut[1] = 0;  // (iterations: debug builds)
+#if RF_DEBUG
+        printf("k_resolve_fix mode %d qn %d Tn %d: %d iterations, %d rescans, %d accepted\n", MODE, J.qn, Tn, dbgIt,
+               dbgRes, s_nacc);
+#endif
     }
 }
 
@@ -1496,13 +1533,14 @@ int launch_grid(const Call& C, const DView& d) {
 
 // Scratch of a job: qp, topk, cnt (+ outputs).
 struct JobOffs {
-    size_t qp, topk, topx, cnt, out, nOut;
+    size_t qp, topk, topx, kval, cnt, out, nOut;
 };
 JobOffs plan_job(Arena& A, int qn, int outN) {
     JobOffs o{};
     o.qp = A.take((size_t)std::max(qn, 1) * sizeof(QP));
-    o.topk = A.take((size_t)std::max(qn, 1) * TOPK * 4);
-    o.topx = A.take((size_t)std::max(qn, 1) * TOPK * 4);
+    o.topk = A.take((size_t)std::max(qn, 1) * TOPK_FIX * 4);
+    o.topx = A.take((size_t)std::max(qn, 1) * TOPK_FIX * 4);
+    o.kval = A.take((size_t)std::max(qn, 1) * 4);
     o.cnt = A.take((size_t)std::max(qn, 1) * 4);
     o.out = A.take((size_t)std::max(outN, 1) * 4);
     o.nOut = A.take(16);
@@ -1513,6 +1551,8 @@ void bind_job(const Call& C, Job& J, const JobOffs& o, int qn, int outN) {
     J.qp = C.at<QP>(o.qp);
     J.topk = C.at<uint32_t>(o.topk);
     J.topx = C.at<uint32_t>(o.topx);
+    J.kval = C.at<int>(o.kval);
+    J.topS = TOPK;
     J.cnt = C.at<int>(o.cnt);
     J.out = C.at<int>(o.out);
     J.outN = outN;
@@ -1525,18 +1565,25 @@ int resolve_lds(const Job& J, size_t* bytes) {
     return ORB_OK;
 }
 
-int run_job(const Call& C, const Job& J) {
+int run_job(const Call& C, const Job& J0) {
     hipStream_t s = C.ctx->stream;
+    // the projection-family matchers: the fixed-point resolver where its state fits (it also
+    // takes targets k_resolve's per-target LDS state cannot: 8 B per target instead of 13), fed
+    // TOPK_FIX-entry candidate lists
+    const bool fixMode = J0.outByTarget && (J0.mode == M_LOCAL || (RF_ALL_MODES && (J0.mode == M_WINDOW || J0.mode == M_F2F ||
+                                                                                     J0.mode == M_MOTION || J0.mode == M_RELOC ||
+                                                                                     J0.mode == M_SIM3P)));
+    const bool useFix = fixMode && resolve_fix_lds(J0) <= 150 * 1024;
+    Job J = J0;
+    J.topS = useFix ? RF_TOPK : TOPK;
     if (J.qn > 0) {
         hipLaunchKernelGGL(k_query_prep, dim3((J.qn + 255) / 256), dim3(256), 0, s, J);
-        hipLaunchKernelGGL(k_query_scan, dim3((J.qn + 3) / 4), dim3(256), 0, s, J);
+        if (J.topS == TOPK_FIX)
+            hipLaunchKernelGGL(k_query_scan<TOPK_FIX>, dim3((J.qn + 3) / 4), dim3(256), 0, s, J);
+        else
+            hipLaunchKernelGGL(k_query_scan<TOPK>, dim3((J.qn + 3) / 4), dim3(256), 0, s, J);
     }
-    // SearchByProjection(local): the fixed-point resolver where its state fits (it also takes
-    // targets k_resolve's per-target LDS state cannot: 8 B per target instead of 13)
-    const bool fixMode = J.outByTarget && (J.mode == M_LOCAL || (RF_ALL_MODES && (J.mode == M_WINDOW || J.mode == M_F2F ||
-                                                                                   J.mode == M_MOTION || J.mode == M_RELOC ||
-                                                                                   J.mode == M_SIM3P)));
-    if (fixMode && resolve_fix_lds(J) <= 150 * 1024) {
+    if (useFix) {
         static std::atomic<bool> fix_attr[64] = {};
         if (!fix_attr[C.device].load()) {
 #define SET_FIX_LDS(M) HIPCHK(hipFuncSetAttribute((const void*)k_resolve_fix<M>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024))
@@ -1899,7 +1946,7 @@ int orb_features_in_area(const orb_frame_view_t* view, int keyframe, int q, cons
     J.areaOut = C.at<int>(oOut);
     hipStream_t s = C.ctx->stream;
     hipLaunchKernelGGL(k_query_prep, dim3((q + 255) / 256), dim3(256), 0, s, J);
-    hipLaunchKernelGGL(k_query_scan, dim3((q + 3) / 4), dim3(256), 0, s, J);
+    hipLaunchKernelGGL(k_query_scan<TOPK>, dim3((q + 3) / 4), dim3(256), 0, s, J);
     HIPCHK(hipGetLastError());
     std::vector<int> cnt(q);
     if ((st = C.download(cnt.data(), jo.cnt, (size_t)q * 4)) || (st = C.sync())) return st;
