@@ -1049,8 +1049,8 @@ __global__ void __launch_bounds__(256) k_resolve(Job J) {
 #ifndef RF_DEBUG
 #define RF_DEBUG 0  // 1: iterations / rescans per call printed (experiment builds)
 #endif
-#ifndef RF_TOPK
-#define RF_TOPK TOPK  // TOPK_FIX: 32-entry lists for the fixed-point resolver (fewer exact rescans)
+#ifndef RF_LONG_LISTS
+#define RF_LONG_LISTS 1  // 32-entry lists for the fixed-point resolver except SearchByProjection(local)
 #endif
 #ifndef RF_ALL_MODES
 #define RF_ALL_MODES 1  // 0: the fixed point for SearchByProjection(local) only
@@ -1575,7 +1575,10 @@ int run_job(const Call& C, const Job& J0) {
                                                                                      J0.mode == M_SIM3P)));
     const bool useFix = fixMode && resolve_fix_lds(J0) <= 150 * 1024;
     Job J = J0;
-    J.topS = useFix ? RF_TOPK : TOPK;
+    // (32 entries: no exact rescan left in the motion-model projection / WindowSearch of the
+    // latency probe, 173 / 301 per call with 8; the local-map search has none with 8 and pays
+    // ~4 us for the longer merge)
+    J.topS = useFix && RF_LONG_LISTS && J0.mode != M_LOCAL ? TOPK_FIX : TOPK;
     if (J.qn > 0) {
         hipLaunchKernelGGL(k_query_prep, dim3((J.qn + 255) / 256), dim3(256), 0, s, J);
         if (J.topS == TOPK_FIX)
