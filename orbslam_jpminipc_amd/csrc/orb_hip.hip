@@ -2832,6 +2832,9 @@ struct MatchGeom {
 #define KM_THREADS 512  // one workgroup (8 waves) per pair: at most a few pairs share a CU
 #endif
 #define KM_WIDE_PAIRS 256  // fewer pairs: 16-wave workgroups (phase 1: NT / 256 lanes per query)
+#ifndef KM_WIDE_ALL
+#define KM_WIDE_ALL 0  // 1: 16-wave workgroups (and the fixed-point phase 2) for every batch
+#endif
 #define MATCH_BIG_NMAX 8192
 #ifndef KM_FIX
 #define KM_FIX 1  // 0: the sequential (speculated) phase 2 for every launch
@@ -4992,8 +4995,9 @@ static int sfi_launch(const orb_keypoint_t* d_kps, const uint8_t* d_desc, const 
     int fixOff = 0;
     const size_t fixAt = (match_lds_bytes(cap, nmax) + 15) & ~(size_t)15;
     const size_t fixEnd = fixAt + (size_t)nmax * (2 * 16 + 8 + 2);
-    const int ntLaunch = P < KM_WIDE_PAIRS ? 2 * KM_THREADS : KM_THREADS;
-    if (KM_FIX && (P < KM_WIDE_PAIRS || KM_FIX_BATCH) && nmax <= ntLaunch && fixEnd <= 158 * 1024) {
+    const bool wide = P < KM_WIDE_PAIRS || KM_WIDE_ALL;  // 16-wave workgroups
+    const int ntLaunch = wide ? 2 * KM_THREADS : KM_THREADS;
+    if (KM_FIX && (wide || KM_FIX_BATCH) && nmax <= ntLaunch && fixEnd <= 158 * 1024) {
         fixOff = (int)fixAt;
         lds = std::max(lds, fixEnd);
     }
@@ -5018,7 +5022,7 @@ static int sfi_launch(const orb_keypoint_t* d_kps, const uint8_t* d_desc, const 
         lk.lock();     // held until the launch that uses it is enqueued
         if (int r = match_big_scratch_locked(st, match_big_slot_bytes(cap, nmaxBig) * (size_t)P, &big)) return r;
     }
-    if (P < KM_WIDE_PAIRS)
+    if (wide)
         hipLaunchKernelGGL(k_match_init<2 * KM_THREADS>, dim3(P), dim3(2 * KM_THREADS), lds, st, A, (uint8_t*)big, nmaxBig);
     else
         hipLaunchKernelGGL(k_match_init<KM_THREADS>, dim3(P), dim3(KM_THREADS), lds, st, A, (uint8_t*)big, nmaxBig);
