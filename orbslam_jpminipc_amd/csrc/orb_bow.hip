@@ -45,6 +45,17 @@ constexpr int BOW_WAVES = 16;  // waves per pair: the common nodes are dealt rou
 constexpr int BOW_T = 64 * BOW_WAVES;
 
 __device__ __forceinline__ uint32_t wmin(uint32_t v) { return orbdev::wave_min_u32(v); }
+// minimum over each 16-lane DPP row, in every lane of the row (row_ror 1, 2, 4, 8)
+__device__ __forceinline__ uint32_t rmin16(uint32_t v) {
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x121, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x122, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x124, 0xF, 0xF, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x128, 0xF, 0xF, false));
+    return v;
+}
+#ifndef BOW_BATCH4
+#define BOW_BATCH4 0  // 1: nodes of <= 16 candidates, four queries per step (speculated, exact)
+#endif
 
 __device__ __forceinline__ int rot_bin(float a1, float a2) {  // ORBmatcher.cc:230-236 / 799-805
     float rot = a1 - a2;
@@ -168,6 +179,88 @@ __global__ void __launch_bounds__(BOW_T) k_bow_pairs(BowBatch J) {
         if (b < 0) continue;
         const int q0 = OA[a], q1 = OA[a + 1], c0 = OB[b], nc = OB[b + 1] - c0;
         if (nc <= 0) continue;
+        if (BOW_BATCH4 && nc <= 16) {
+            // Four queries per step, lane 16g + c: query g of the step against candidate c (each
+            // of the four 16-lane rows holds the node's candidates and their matched flags).  A
+            // query's outcome is fixed by its best and second unmatched candidates and an
+            // acceptance marks exactly one candidate, so the step's queries are decided from the
+            // step-start state unless an earlier query of the step accepted one of them (the
+            // speculation of k_resolve / k_match_init): the step commits its queries before the
+            // first such one, at least one per step.
+            const int c = lane & 15, g = lane >> 4;
+            int myIdx = 0;
+            uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
+            bool myTaken = true;
+            if (c < nc) {
+                myIdx = min((unsigned)FB[c0 + c], (unsigned)(nB - 1));
+                m0 = DB[2 * (size_t)myIdx];
+                m1 = DB[2 * (size_t)myIdx + 1];
+                myTaken = s_taken[myIdx] != 0;
+            }
+            int qIdx = 0, qOk = 0, base = q0 - 64;
+            uint4 qd0 = make_uint4(0, 0, 0, 0), qd1 = qd0;
+            for (int q = q0; q < q1;) {
+                if (q + 4 > base + 64) {  // the next 64 queries, one per lane
+                    base = q;
+                    qOk = 0;
+                    if (q + lane < q1) {
+                        qIdx = FA[q + lane];
+                        qOk = (unsigned)qIdx < (unsigned)nA && (!UA || UA[qIdx]);  // !pMP || pMP->isBad()
+                        const int qi = qOk ? qIdx : 0;
+                        qd0 = DA[2 * (size_t)qi];
+                        qd1 = DA[2 * (size_t)qi + 1];
+                    }
+                }
+                const int src = q - base + g;  // < 64
+                // (every lane takes part in each ds_bpermute: a lane that is inactive for one
+                // provides no source data, so none of these sits behind a per-lane condition)
+                const int okS = __shfl(qOk, src, 64);
+                const bool okG = q + g < q1 && okS != 0;
+                uint4 d0, d1;
+                d0.x = (uint32_t)__shfl((int)qd0.x, src, 64), d0.y = (uint32_t)__shfl((int)qd0.y, src, 64);
+                d0.z = (uint32_t)__shfl((int)qd0.z, src, 64), d0.w = (uint32_t)__shfl((int)qd0.w, src, 64);
+                d1.x = (uint32_t)__shfl((int)qd1.x, src, 64), d1.y = (uint32_t)__shfl((int)qd1.y, src, 64);
+                d1.z = (uint32_t)__shfl((int)qd1.z, src, 64), d1.w = (uint32_t)__shfl((int)qd1.w, src, 64);
+                const uint32_t key = okG && !myTaken ? ((uint32_t)ham(d0, d1, m0, m1) << 16) | (uint32_t)c : NONE;
+                const uint32_t b1 = rmin16(key);
+                const uint32_t b2 = rmin16(key == b1 ? NONE : key);
+                bool accept = false;
+                if (b1 != NONE) {
+                    const int dist1 = (int)(b1 >> 16);
+                    const int dist2 = b2 == NONE ? INT_MAX : (int)(b2 >> 16);
+                    const bool thOk = J.kfkf ? dist1 < TH_LOW : dist1 <= TH_LOW;
+                    accept = thOk && (float)dist1 < J.nnratio * (float)dist2;
+                }
+                const int bc = b1 != NONE ? (int)(b1 & 0xFFFFu) : -1, sc = b2 != NONE ? (int)(b2 & 0xFFFFu) : -2;
+                const uint64_t accM = __ballot(accept && c == 0);  // bit 16g: query g accepts
+                int bcG[4];
+#pragma unroll
+                for (int h = 0; h < 4; ++h) bcG[h] = __builtin_amdgcn_readlane(bc, 16 * h);
+                bool hit = false;
+#pragma unroll
+                for (int h = 0; h < 3; ++h)
+                    hit |= h < g && ((accM >> (16 * h)) & 1ull) && (bcG[h] == bc || bcG[h] == sc);
+                const uint64_t stopM = __ballot(hit && c == 0);
+                const int nb = min(4, q1 - q);
+                const int jstop = stopM ? min((__ffsll((unsigned long long)stopM) - 1) >> 4, nb) : nb;
+#pragma unroll
+                for (int h = 0; h < 4; ++h) {
+                    if (h >= jstop || !((accM >> (16 * h)) & 1ull)) continue;  // (wave-uniform)
+                    if (c == bcG[h]) myTaken = true;
+                    if (lane == 0) {
+                        const int idx1 = __builtin_amdgcn_readlane(qIdx, q - base + h);
+                        const int idx2 = __builtin_amdgcn_readlane(myIdx, bcG[h]);
+                        if (J.kfkf)
+                            out[idx1] = idx2;
+                        else
+                            out[idx2] = idx1;
+                        ++acc;
+                    }
+                }
+                q += jstop;
+            }
+            continue;
+        }
         const bool small = nc <= 64;
         // <= 64 candidates: one per lane, descriptor held for the whole node
         int myIdx = 0;
