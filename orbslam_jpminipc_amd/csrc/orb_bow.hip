@@ -54,7 +54,7 @@ __device__ __forceinline__ uint32_t rmin16(uint32_t v) {
     return v;
 }
 #ifndef BOW_BATCH4
-#define BOW_BATCH4 0  // 1: nodes of <= 16 candidates, four queries per step (speculated, exact)
+#define BOW_BATCH4 1  // nodes of <= 16 candidates: four queries per step (speculated, exact); 0: one per step
 #endif
 
 __device__ __forceinline__ int rot_bin(float a1, float a2) {  // ORBmatcher.cc:230-236 / 799-805
