@@ -37,6 +37,19 @@
 #include "orb_device.h"
 #include "pattern31.inc"
 
+// Translation units: orb_ilp.hip compiles this file again (ORB_TU_ILP) for k_fast and
+// k_pyr_stream alone, under the max-ILP machine scheduler; this unit then leaves those two out
+// and launches them through orb_ilp.hip's launchers.  ORB_ILP_SPLIT 0 keeps both here (the
+// timing builds do: their probe symbols live in this unit).
+#ifdef ORB_TU_ILP
+#define ORB_TU_MAIN 0
+#else
+#define ORB_TU_MAIN 1
+#endif
+#ifndef ORB_ILP_SPLIT
+#define ORB_ILP_SPLIT (!KF_TIMING && !PS_TIMING)
+#endif
+#define ORB_ILP_HERE (ORB_TU_MAIN != ORB_ILP_SPLIT)  // k_fast / k_pyr_stream defined in this unit
 #define ORB_MAX_LEVELS 16
 #define ORB_MAX_CELLS_PER_LEVEL 256
 #define ORB_SELECT_LDS_CAP 6144
@@ -47,7 +60,9 @@
 #define KR_TIMING 0
 #endif
 #if KR_TIMING
+#if ORB_TU_MAIN
 __device__ unsigned long long g_krtime[ORB_MAX_LEVELS][8];
+#endif
 #define KR_T(i) const unsigned long long krt##i = __builtin_amdgcn_s_memrealtime()
 #else
 #define KR_T(i)
@@ -56,7 +71,9 @@ __device__ unsigned long long g_krtime[ORB_MAX_LEVELS][8];
 #define KS_TIMING 0
 #endif
 #if KS_TIMING
+#if ORB_TU_MAIN
 __device__ unsigned long long g_kstime[ORB_MAX_LEVELS][8];
+#endif
 #define KS_T(i) const unsigned long long kst##i = __builtin_amdgcn_s_memrealtime()
 #else
 #define KS_T(i)
@@ -77,6 +94,7 @@ __device__ unsigned long long g_kftime[8];
 // ======================================================================================
 // error plumbing
 // ======================================================================================
+#if ORB_TU_MAIN
 static thread_local std::string g_last_error = "";
 
 int orb_internal_set_error(int code, const std::string& msg) {
@@ -85,6 +103,7 @@ int orb_internal_set_error(int code, const std::string& msg) {
 }
 
 static int set_err(int code, const std::string& msg) { return orb_internal_set_error(code, msg); }
+#endif
 
 #define HIP_TRY(expr)                                                                               \
     do {                                                                                            \
@@ -158,6 +177,7 @@ __device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t a, uint32_t b) {
     return r;
 }
 
+#if ORB_TU_MAIN  // (none of them is read by k_fast / k_pyr_stream)
 // bit_pattern_31_ (ORBextractor.cc:197-455) as floats, pair-major: c_patternf[2 (64 q + l) + {0, 1}]
 // = (x, y) of point 8 l + q, i.e. lane l's eight points are one float2 in each of eight 512-B
 // rows (k_orient_desc loads each row with one fully coalesced global_load_dwordx2, §6.1)
@@ -178,11 +198,13 @@ __constant__ uint4 c_rowB[4 * 64];  // 279 patch dwords per alignment, zero-padd
 // weight tap[d] (x 256 for the high byte), d = delta + 4h + (j & 3) - o, delta = the M-tile's
 // first row minus the block's (v 0: 0, v 1: 16, v 2: 12 without the tile's rows 0 .. 3)
 __constant__ uint4 c_colA[3 * 64];
+#endif
 // ---- pyramid --------------------------------------------------------------------------
 // Level 0: copyMakeBorder(image, 16, BORDER_REFLECT_101); one thread per 16-byte chunk of a
 // padded row (pitch is a multiple of 16).  Interior chunks (source columns [x-16, x) inside the
 // row) are one 16-, four 4- or sixteen 1-byte loads depending on the source alignment and one
 // 16-byte store; the two border chunks per side reflect byte by byte.
+#if ORB_TU_MAIN
 __global__ void __launch_bounds__(256) k_pyr0(const uint8_t* __restrict__ imgs, int stride, long long fpitch,
                                               uint8_t* __restrict__ pyr, Geom g) {
     const LevelGeom& lg = g.lv[0];
@@ -227,11 +249,13 @@ __global__ void __launch_bounds__(256) k_pyr0(const uint8_t* __restrict__ imgs, 
     }
     *(uint4*)(pyr + lg.base + (long long)b * lg.fstride + (long long)py * lg.pitch + x16) = out;
 }
+#endif  // ORB_TU_MAIN
 
 // Level 0 from 3- or 4-channel frames: Tracking::GrabImage's cvtColor(.., CV_RGB2GRAY /
 // CV_BGR2GRAY) (Tracking.cc:202-207) fused with the padding.  OpenCV 2.4's RGB2Gray<uchar> is an
 // exact fixed-point sum, (c0*p[0] + 9617*p[1] + c2*p[2] + 2^13) >> 14 with R2Y = 4899,
 // G2Y = 9617, B2Y = 1868 (yuv_shift 14): (c0, c2) = (R2Y, B2Y) for RGB order, (B2Y, R2Y) for BGR.
+#if ORB_TU_MAIN
 __global__ void __launch_bounds__(256) k_pyr0_color(const uint8_t* __restrict__ imgs, int stride, long long fpitch,
                                                     int cn, int c0, int c2, uint8_t* __restrict__ pyr, Geom g) {
     const LevelGeom& lg = g.lv[0];
@@ -252,6 +276,7 @@ __global__ void __launch_bounds__(256) k_pyr0_color(const uint8_t* __restrict__ 
     }
     *(uint32_t*)(pyr + lg.base + (long long)b * lg.fstride + (long long)py * lg.pitch + x4) = word;
 }
+#endif  // ORB_TU_MAIN
 
 // Stage `rows` x `units` 16-byte units (global row pitch gsu units, LDS row pitch the same
 // `units`) with 256 threads, up to RZ_SB units per thread all in flight before any LDS write:
@@ -311,6 +336,7 @@ __device__ __forceinline__ void stage_tile16(uint4* __restrict__ dst, const uint
 #endif
 // The two levels arrive by value: a Geom indexed by the runtime level was copied to scratch
 // (144 B per lane of private-memory traffic per thread).
+#if ORB_TU_MAIN
 template <int TH>
 __global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, const int* __restrict__ rtab,
                                                     const LevelGeom lg, const LevelGeom ls) {
@@ -430,6 +456,7 @@ __global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, c
         }
     }
 }
+#endif  // ORB_TU_MAIN
 
 // Levels lf .. L-1 of one frame per 1024-thread workgroup (the small levels: one launch
 // instead of one per level, each of which was latency-bound at a few thousand pixels per
@@ -443,6 +470,7 @@ __global__ void __launch_bounds__(256) k_pyr_resize(uint8_t* __restrict__ pyr, c
 #ifndef KR_TAIL  // 0: every level by k_pyr_resize (experiment switch)
 #define KR_TAIL 1
 #endif
+#if ORB_TU_MAIN
 __global__ void __launch_bounds__(RT_THREADS) k_pyr_resize_tail(uint8_t* __restrict__ pyr,
                                                                 const int* __restrict__ rtab, Geom g, int lf,
                                                                 int bufA, int bufB) {
@@ -533,6 +561,7 @@ __global__ void __launch_bounds__(RT_THREADS) k_pyr_resize_tail(uint8_t* __restr
         __syncthreads();  // level l complete in LDS; the tables are free
     }
 }
+#endif  // ORB_TU_MAIN
 
 // ---- the whole pyramid of a frame in one streaming pass (large batches) ------------------
 // k_pyr0 + k_pyr_resize x (L-1) read every level l-1 back from HBM to build level l.  Here one
@@ -645,6 +674,7 @@ __device__ unsigned long long g_pstime[32];
 #define PS_WAVES 8  // waves per SIMD the register allocation targets (two workgroups per CU)
 #endif
 #define PS_LB 4  // level-0 units per loader lane in flight at once
+#if ORB_ILP_HERE
 __global__ void __launch_bounds__(PS_THREADS) __attribute__((amdgpu_waves_per_eu(PS_WAVES)))
 k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uint8_t* __restrict__ pyr,
              const uint32_t* __restrict__ colWords, const uint4* __restrict__ rowEntries,
@@ -915,6 +945,7 @@ k_pyr_stream(const uint8_t* __restrict__ imgs, int stride, long long fpitch, uin
     }
 #endif
 }
+#endif  // ORB_ILP_HERE
 
 typedef short i16x2 __attribute__((ext_vector_type(2)));
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
@@ -1347,6 +1378,7 @@ __device__ int cell_fast_rerun(const uint8_t* __restrict__ det, int pitch, int d
                     // B = 512 with 2 / 3 / 5 / 6 / 8: 1241x376 0.406 / 0.404 / 0.434 / 0.437 /
                     // 0.453 ms vs 0.357, 1280x720 0.90-1.17 vs 0.765
 #endif
+#if ORB_TU_MAIN
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KR_WAVES))) k_rerun(const uint8_t* __restrict__ pyr, uint32_t* __restrict__ cand,
                                                int* __restrict__ cellCount, Geom g,
                                                const CellGeom* __restrict__ cells, int NWG) {
@@ -1385,6 +1417,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KR_WAV
         }
     }
 }
+#endif  // ORB_TU_MAIN
 
 // ---- selection (retainBest replay) -------------------------------------------------------
 struct ScoreGreater {  // KeypointResponseGreater on the packed FAST score
@@ -1518,6 +1551,7 @@ __device__ __forceinline__ void select_frame_done(int b, int L, int l, int keep,
     __hip_atomic_store(&selDone[b], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+#if ORB_TU_MAIN
 template <bool HARRIS, bool RERUN>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAVES))) k_select(const uint8_t* __restrict__ pyr, uint32_t* __restrict__ cand,
                                                 uint32_t* __restrict__ cand2, int* __restrict__ cellCount, Geom g,
@@ -1826,6 +1860,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KS_WAV
     }
 #endif
 }
+#endif  // ORB_TU_MAIN
 
 // ---- FAST on the levels: per-tile detection + the per-cell non-max suppression --------------
 // ComputeKeyPoints runs cv::FAST(cellImage, keys, fastTh, true) on every cell ROI of every
@@ -1882,6 +1917,7 @@ struct FastTile {
 #if KF_B64
 static_assert(KF_DPL == 2, "KF_B64 reads the groups' dword pairs");
 #endif
+#if ORB_ILP_HERE
 __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, Geom g,
                                                       const FastTile* __restrict__ tiles,
                                                       uint32_t* __restrict__ cand, int* __restrict__ cellCount) {
@@ -2293,6 +2329,7 @@ __global__ void __launch_bounds__(256) k_fast(const uint8_t* __restrict__ pyr, G
     }
 #endif
 }
+#endif  // ORB_ILP_HERE
 
 // ---- orientation + descriptor -------------------------------------------------------------
 // One wave per keypoint slot.  Two memory round trips per wave: (1) the slot's packed record
@@ -2379,6 +2416,7 @@ typedef float od_f32x4 __attribute__((ext_vector_type(4)));
 #else
 #define OD_ATTR
 #endif
+#if ORB_TU_MAIN
 __global__ void __launch_bounds__(64 * OD_WAVES) OD_ATTR k_orient_desc(const uint8_t* __restrict__ pyr, Geom g,
                                                      const uint32_t* __restrict__ lvlOut,
                                                      const uint8_t* __restrict__ slotLvl,
@@ -2775,10 +2813,12 @@ __global__ void __launch_bounds__(64 * OD_WAVES) OD_ATTR k_orient_desc(const uin
         kps[kslot] = kp;
     }
 }
+#endif  // ORB_TU_MAIN
 
 // The descriptor image of one level (blurred ROI + raw border), over level coordinates
 // [-3, ringX1) x [-3, ringY1), by the same row / column passes and rounding as k_orient_desc:
 // test hook behind orb_debug_blur_image (not on the product path).  One thread per pixel.
+#if ORB_TU_MAIN
 __global__ void __launch_bounds__(256) k_debug_desc_image(const uint8_t* __restrict__ pyr, LevelGeom lg, int b,
                                                           uint8_t* __restrict__ out) {
     const int i = blockIdx.x * 256 + threadIdx.x;
@@ -2799,6 +2839,7 @@ __global__ void __launch_bounds__(256) k_debug_desc_image(const uint8_t* __restr
     }
     out[i] = (uint8_t)v;
 }
+#endif  // ORB_TU_MAIN
 
 // ---- SearchForInitialization ------------------------------------------------------------
 struct MatchGeom {
@@ -2852,7 +2893,9 @@ struct MatchGeom {
 #define KM_TIMING 0
 #endif
 #if KM_TIMING
+#if ORB_TU_MAIN
 __device__ unsigned long long g_kmtime[8];
+#endif
 #define KM_T(i) const unsigned long long kmt##i = __builtin_amdgcn_s_memrealtime()
 #else
 #define KM_T(i)
@@ -3589,6 +3632,7 @@ __device__ __forceinline__ bool match_pair(const MatchArgs& A, int p, int nmax, 
 // NT threads: KM_THREADS (8 waves) when pairs share CUs; 16 waves when each pair has a CU to
 // itself (fewer pairs than KM_WIDE_PAIRS, e.g. one SearchForInitialization call): phase 1 then
 // scores each query with four lanes instead of two.
+#if ORB_TU_MAIN
 template <int NT>
 __global__ void __launch_bounds__(NT) k_match_init(MatchArgs A, uint8_t* __restrict__ big, int nmaxBig) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -3607,10 +3651,22 @@ __global__ void __launch_bounds__(NT) k_match_init(MatchArgs A, uint8_t* __restr
         }
     }
 }
+#endif  // ORB_TU_MAIN
 
 // ======================================================================================
 // host side
 // ======================================================================================
+#if ORB_TU_MAIN
+#if ORB_ILP_SPLIT
+// orb_ilp.hip's launchers of its k_pyr_stream / k_fast (library-internal)
+__attribute__((visibility("hidden"))) void orb_ilp_init();
+__attribute__((visibility("hidden"))) void orb_ilp_pyr_stream(int B, size_t lds, hipStream_t st, const uint8_t* imgs, int stride, long long fpitch,
+                        uint8_t* pyr, const uint32_t* scol, const uint4* srows, const StreamLevel* slv,
+                        const uint32_t* srounds, const StreamGeom& sg, int* cellCount, int nCells);
+__attribute__((visibility("hidden"))) void orb_ilp_fast(int nTiles, int B, hipStream_t st, const uint8_t* pyr,
+                                                       const Geom& g, const FastTile* tiles, uint32_t* cand,
+                                                       int* cellCount);
+#endif
 namespace {
 
 inline int cvRoundH(double v) { return (int)lrint(v); }
@@ -4481,9 +4537,15 @@ struct orb_extractor {
             StreamGeom sg = sgeom;
             const uintptr_t al = (uintptr_t)d_imgs | (uintptr_t)stride | (uintptr_t)fpitch;
             sg.align = (al & 15u) == 0 ? 16 : (al & 3u) == 0 ? 4 : 1;
+#if ORB_ILP_SPLIT
+            orb_ilp_pyr_stream(B, streamLds, st, d_imgs, stride, fpitch, d_pyr, (const uint32_t*)d_scol,
+                               (const uint4*)d_srows, (const StreamLevel*)d_slv, (const uint32_t*)d_srounds, sg,
+                               (phases & 2u) ? d_cellCount : (int*)nullptr, g.nCells);
+#else
             hipLaunchKernelGGL(k_pyr_stream, dim3(B), dim3(PS_THREADS), streamLds, st, d_imgs, stride, fpitch, d_pyr,
                                (const uint32_t*)d_scol, (const uint4*)d_srows, (const StreamLevel*)d_slv,
                                (const uint32_t*)d_srounds, sg, (phases & 2u) ? d_cellCount : (int*)nullptr, g.nCells);
+#endif
             countsZeroed = (phases & 2u) != 0;
             stage_end(0, st);
             pyrBatch = B;
@@ -4528,7 +4590,11 @@ struct orb_extractor {
         }
         stage_begin(2, st);
         if (!countsZeroed) HIP_TRY(hipMemsetAsync(d_cellCount, 0, (size_t)g.nCells * B * 4, st));
+#if ORB_ILP_SPLIT
+        orb_ilp_fast(nTiles, B, st, d_pyr, g, d_tiles, d_cand, d_cellCount);
+#else
         hipLaunchKernelGGL(k_fast, dim3(nTiles, B), dim3(256), 0, st, d_pyr, g, d_tiles, d_cand, d_cellCount);
+#endif
         stage_end(2, st);
         stage_begin(3, st);
         // FAST(7) re-runs: spread over NWG workgroups per level first (k_rerun), or inside
@@ -4686,7 +4752,11 @@ int orb_extractor_create(int nfeatures, float scale_factor, int nlevels, int sco
     hipFuncSetAttribute((const void*)k_select<false, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
     hipFuncSetAttribute((const void*)k_rerun, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
     hipFuncSetAttribute((const void*)k_pyr_resize_tail, hipFuncAttributeMaxDynamicSharedMemorySize, RT_LDS_MAX);
+#if ORB_ILP_SPLIT
+    orb_ilp_init();
+#else
     hipFuncSetAttribute((const void*)k_pyr_stream, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+#endif
     orb_extractor* h = new orb_extractor();
     h->nfeatures = nfeatures;
     h->scaleFactor = scale_factor;
@@ -5314,3 +5384,4 @@ int orb_debug_cell_counts(orb_extractor_t* h, int b, int l, int* counts, int cap
 }
 
 }  // extern "C"
+#endif  // ORB_TU_MAIN (host side)

@@ -25,27 +25,26 @@ src.write_text(s.replace('#include "../../include/', '#include "../include/'))
 for f in (tmp / "csrc").glob("*.hip"):
     t = f.read_text().replace('"../../include/', '"../include/')
     f.write_text(t)
-units = [tmp / "csrc" / u for u in ("orb_hip.hip", "orb_match.hip", "orb_voc.hip", "orb_mappoint.hip",
-                                    "orb_pipeline.hip", "orb_persist.hip", "orb_frame.hip", "orb_bow.hip")]
+sys.path.insert(0, str(ROOT))
+from __graft_entry__ import HIPCC_FLAGS, build_lib, hipcc_flags  # noqa: E402  (the library's recipe)
+
 out = ROOT / "build" / "variants" / f"{name}.so"
 out.parent.mkdir(parents=True, exist_ok=True)
-sys.path.insert(0, str(ROOT))
-from __graft_entry__ import hipcc_flags  # noqa: E402  (the library's flags, optional ones probed)
-
-flags = hipcc_flags()
-if os.environ.get("ORB_VARIANT_NO_OPT"):  # without the probed OPTIONAL_FLAGS (-amdgpu-mfma-vgpr-form=1)
-    from __graft_entry__ import HIPCC_FLAGS  # noqa: E402
-    flags = list(HIPCC_FLAGS)
-flags = flags + os.environ.get("ORB_VARIANT_EXTRA", "").split()
+extra = os.environ.get("ORB_VARIANT_EXTRA", "").split()
 if os.environ.get("ORB_VARIANT_ASM"):  # device assembly of orb_hip.hip only: build/variants/NAME.s
-    flags = [f for f in flags if f not in ("-shared", "-fPIC")] + os.environ.get("ORB_VARIANT_FLAGS", "").split()
+    flags = [f for f in hipcc_flags() + extra if f not in ("-shared", "-fPIC")] + \
+        os.environ.get("ORB_VARIANT_FLAGS", "").split()
     out = out.with_suffix(".s")
-    r = subprocess.run(["/opt/rocm/bin/hipcc", *flags, "--cuda-device-only", "-S", "-o", str(out), str(units[0])],
-                       capture_output=True, text=True)
+    r = subprocess.run(["/opt/rocm/bin/hipcc", *flags, "--cuda-device-only", "-S", "-o", str(out),
+                        str(tmp / "csrc" / "orb_hip.hip")], capture_output=True, text=True)
     shutil.rmtree(tmp)
     sys.exit(r.stderr[-3000:] if r.returncode else print("asm", out))
-r = subprocess.run(["/opt/rocm/bin/hipcc", *flags, "-o", str(out), *map(str, units)], capture_output=True, text=True)
-shutil.rmtree(tmp)
-if r.returncode:
-    sys.exit(r.stderr[-3000:])
+if os.environ.get("ORB_VARIANT_NO_OPT"):  # without the probed OPTIONAL_FLAGS (-amdgpu-mfma-vgpr-form=1)
+    import __graft_entry__  # noqa: E402
+
+    __graft_entry__.hipcc_flags = lambda hipcc="": list(HIPCC_FLAGS)
+try:
+    build_lib(out, tmp / "csrc", extra)
+finally:
+    shutil.rmtree(tmp)
 print("built", out)

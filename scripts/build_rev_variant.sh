@@ -10,6 +10,10 @@ git archive "$REV" orbslam_jpminipc_amd/csrc include | tar -x -C "$T"
 F="$(python3 __graft_entry__.py flags)"  # the library's own flags (optional ones probed)
 mkdir -p build/variants
 C=$T/orbslam_jpminipc_amd/csrc
-/opt/rocm/bin/hipcc $F -o build/variants/$NAME.so $C/orb_hip.hip $C/orb_match.hip $C/orb_voc.hip $C/orb_mappoint.hip $C/orb_pipeline.hip $C/orb_persist.hip $C/orb_frame.hip $C/orb_bow.hip 2> build/variants/$NAME.log
+if [ -f $C/orb_ilp.hip ]; then  # revisions with the max-ILP unit: the library's own recipe
+    python3 __graft_entry__.py lib build/variants/$NAME.so $C 2> build/variants/$NAME.log
+else
+    /opt/rocm/bin/hipcc $F -o build/variants/$NAME.so $C/orb_hip.hip $C/orb_match.hip $C/orb_voc.hip $C/orb_mappoint.hip $C/orb_pipeline.hip $C/orb_persist.hip $C/orb_frame.hip $C/orb_bow.hip 2> build/variants/$NAME.log
+fi
 rm -rf "$T"
 echo "built build/variants/$NAME.so from $REV"

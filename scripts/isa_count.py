@@ -1,11 +1,13 @@
 #!/usr/bin/env python3
 """Static instruction counts per kernel of a HIP source (device assembly for gfx950).
 
-Usage: isa_count.py [SRC] [-DFLAG=V ...] [KERNEL_SUBSTR ...]   (default SRC: csrc/orb_hip.hip, all kernels)
+Usage: isa_count.py [SRC] [-DFLAG=V ...] [KERNEL_SUBSTR ...]   (default SRC: csrc/orb_hip.hip, all kernels;
+extra compiler options, e.g. -mllvm ones, in $ISA_EXTRA)
 Prints per kernel: VALU / SALU / LDS / VMEM / SMEM / MFMA counts, VGPRs, SGPRs, LDS bytes and
 the occupancy the compiler reports.  Static counts (each instruction once, loops not unrolled at
 run time): a quick CPU-side check of a kernel edit before it is timed on the GPU."""
 import collections
+import os
 import pathlib
 import re
 import subprocess
@@ -20,7 +22,7 @@ src = pathlib.Path(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].endswith(".
     ROOT / "orbslam_jpminipc_amd" / "csrc" / "orb_hip.hip"
 keys = [a for a in sys.argv[1:] if not a.endswith(".hip") and not a.startswith("-D")]
 flags = [f for f in hipcc_flags() if f not in ("-shared", "-fPIC")] + [
-    a for a in sys.argv[1:] if a.startswith("-D")]
+    a for a in sys.argv[1:] if a.startswith("-D")] + os.environ.get("ISA_EXTRA", "").split()
 with tempfile.TemporaryDirectory() as d:
     out = pathlib.Path(d) / "k.s"
     subprocess.run(["/opt/rocm/bin/hipcc", *flags, "--cuda-device-only", "-S", "-o", str(out), str(src)], check=True)
