@@ -5,8 +5,9 @@
 // Both kernels' occupancy is set by LDS (k_fast: five workgroups per CU) or by their own
 // waves-per-EU target (k_pyr_stream: two workgroups per CU), so the default scheduler's
 // occupancy-first schedule gains nothing from the registers it saves, and both kernels' time is
-// their instruction issue: k_fast 441.8 -> 435.1 us, k_pyr_stream 289.6 -> 286.1 us per c3 step
-// on one box (profiles/r06/r06_ilp2_summary.txt; HISTORY.md round 6).  The rest of
+// their instruction issue: k_fast 442.5 -> 437.5 us per c3 step on one box, k_pyr_stream
+// unchanged (289.4 / 289.9 us; both orders, two copies each: profiles/r06/r06_ilp3_summary.txt,
+// HISTORY.md round 6).  The rest of
 // the library keeps the default: k_orient_desc under max-ILP takes 112 VGPRs (occupancy 8 -> 4,
 // 0.43 -> 0.58 ms) and spills when held to eight waves; k_select measured 10 % slower.
 //
